@@ -1,0 +1,269 @@
+/*
+ * qsc.h — C ABI of libqsc_hip.so, the MI355X (gfx950) hot path of the one-bit / quantized
+ * maximum-likelihood tensor factorisation of shresthasagar/quantized_spectrum_cartography.
+ *
+ * The reference has no native boundary: its hot path is module-level Python on torch CPU
+ * tensors (qmc/quantization_model.py, qmc/quantization_model_log.py) driven by the alternating
+ * solver in qmc/qmc.ipynb cell 1 (raw-JSON lines :559-645).  Each entry point below names the
+ * reference function it replaces (file:line).  The Python package
+ * quantized_spectrum_cartography_amd binds these symbols with ctypes.
+ *
+ * Conventions
+ *   - every pointer argument is DEVICE memory owned by the caller (contiguous, naturally
+ *     aligned), except arguments documented as host pointers (qsc_model*, qsc_obs_desc*);
+ *   - the library never allocates device memory: callers size workspaces with the
+ *     *_workspace_bytes() queries;
+ *   - every call is asynchronous on the given hipStream_t (passed as void*), except the two
+ *     calls documented as synchronous (qsc_obs_layout, qsc_device_check);
+ *   - return value: 0 on success, QSC_EINVAL on a bad argument, otherwise a hipError_t.
+ *
+ * Tensor layouts (fp32 unless stated; "pixel" p = i*J + j, P = I*J):
+ *   S   [R][P]        emitter spatial loss fields   (reference S: (R,1,I,J))
+ *   C   [R][K]        emitter power spectra         (reference C: (R,K))
+ *   T   [K][P]        radio map T = sum_r S_r (x) c_r (reference get_tensor output (K,I,J))
+ *   Y   [K][P] int64  bin indices                   (reference quantize output)
+ *   codes [K][P] u8   Y with the sampling mask folded in: 0xFF = unobserved
+ */
+#ifndef QSC_H_
+#define QSC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QSC_API __attribute__((visibility("default")))
+
+#define QSC_OK 0
+#define QSC_EINVAL 100000
+#define QSC_MAX_BOUNDS 256 /* nbins <= 255: code 0xFF is the "unobserved" sentinel */
+#define QSC_MAX_R 16       /* rank bound of the fused passes */
+#define QSC_UNOBSERVED 0xFF
+
+/* Probit observation model, host struct passed by pointer.
+ *   reference: F_probit qmc/quantization_model.py:57-61 (constant 1.414213, kept verbatim);
+ *              prob_probit qmc/quantization_model.py:22-39 (linear: b[0]=-1e5, b[-1]=1e5 clamp)
+ *              and qmc/quantization_model_log.py:23-41 (log model: no clamp);
+ *              quantize qmc/quantization_model.py:8-20 / _log.py:9-21 (b[-1]=inf).
+ * sigma and offset are doubles because the reference passes Python floats: the library forms
+ * fp32(sigma*1.414213) and fp32(offset) exactly as torch does for a tensor-scalar op. */
+typedef struct qsc_model {
+  int32_t nbounds;   /* number of bin boundaries = nbins + 1, 2..QSC_MAX_BOUNDS */
+  int32_t log_model; /* 0: linear model, 1: log-domain model x = log(t + offset) */
+  double sigma;      /* probit noise standard deviation */
+  double offset;     /* log-model offset (ignored when log_model == 0) */
+  float bounds[QSC_MAX_BOUNDS]; /* bin boundaries as the caller gives them (unclamped) */
+} qsc_model;
+
+/* Adam hyper-parameters (torch.optim.Adam defaults: betas (0.9, 0.999), eps 1e-8).  The
+ * per-step bias corrections are computed on the device from the step counters held in the
+ * solver state, so one captured hipGraph can be replayed for every iteration. */
+typedef struct qsc_adam {
+  double lr; /* doubles: torch forms 1 - beta^step and lr / bc1 in Python floats */
+  double beta1;
+  double beta2;
+  double eps;
+  int32_t project_nonneg; /* apply x[x<0] = 0 after the step (qmc/qmc.ipynb :579) */
+  int32_t pad_;
+} qsc_adam;
+
+/* Device-resident solver scalars (one struct per solve, caller-allocated device memory,
+ * zero-initialised by qsc_state_init). Kernels read and write it; host reads it back only
+ * when it wants the cost history. */
+typedef struct qsc_state {
+  int32_t step_c;   /* Adam steps taken on C */
+  int32_t step_s;   /* Adam steps taken on S */
+  int32_t iter;     /* completed outer iterations */
+  int32_t pad_;
+  float normsq_s;   /* ||S||_F^2 of the current S */
+  float normsq_c;   /* ||C||_F^2 of the current C (before the last C update) */
+  float nll_c;      /* NLL of the last C-pass   (-sum Wx log P, qmc/qmc.ipynb :572) */
+  float nll_s;      /* NLL of the last S-pass */
+  float reserved[8];
+} qsc_state;
+
+/* Packed observation layout, produced by qsc_obs_layout (host struct).
+ * Positions q in 0..Pp-1 are pixels re-ordered by observation count (perm[q] = pixel).
+ *  S-format ("pixel slices"): for slice s (64 positions), lane l, entry j < s_width[s]:
+ *     idx = s_off[s] + (j/4)*256 + l*4 + (j%4);  value = k | code << KBITS  (code PAD = pad)
+ *  C-format ("frequency slices" per pixel tile): tile t (PT positions), k-slice ks (64 k's),
+ *     lane l (k = 64*ks + l), entry j < c_width[t*nks+ks]:
+ *     idx = c_off[t*nks+ks] + (j/4)*256 + l*4 + (j%4);  value = qlocal | code << QBITS
+ *  narrow (wide == 0): uint16 entries, KBITS = QBITS = 12, code PAD = 15 (K, PT <= 4096, nbins <= 15)
+ *  wide   (wide == 1): uint32 entries, KBITS = QBITS = 24, code PAD = 255 */
+typedef struct qsc_obs_desc {
+  int32_t K;      /* frequency bins in this (local) slab */
+  int32_t P;      /* pixels I*J */
+  int32_t Pp;     /* P rounded up to 64 */
+  int32_t PT;     /* C-pass pixel tile (positions), multiple of 64, <= 4096 when narrow */
+  int32_t ntiles; /* Pp / PT */
+  int32_t nks;    /* ceil(K / 64) */
+  int32_t wide;   /* entry width selector, see above */
+  int32_t nbins;  /* number of bins (codes 0..nbins-1) */
+  int64_t nnz;    /* observed entries */
+  int64_t s_entries; /* S-format entries incl. padding */
+  int64_t c_entries; /* C-format entries incl. padding */
+} qsc_obs_desc;
+
+/* ---------------------------------------------------------------------------------------
+ * library / device
+ * ------------------------------------------------------------------------------------- */
+QSC_API int qsc_version(void);
+QSC_API const char* qsc_error_string(int code);
+/* synchronous: returns 0 if device `dev` is a gfx950 the code objects can run on */
+QSC_API int qsc_device_check(int dev);
+
+/* ---------------------------------------------------------------------------------------
+ * elementwise model ops
+ * ------------------------------------------------------------------------------------- */
+/* quantize: qmc/quantization_model.py:8-20 (linear), qmc/quantization_model_log.py:9-21 (log).
+ * noise = torch.randn(X.shape) drawn by the caller (host RNG, as in the reference);
+ * x = X + noise*fp32(sigma) (linear) or log(X + offset) + noise*fp32(sigma) (log);
+ * Y = i for b[i] < x <= b[i+1] (i >= 1, b[-1] = +inf), else 0.                             */
+QSC_API int qsc_quantize(const float* X, const float* noise, int64_t n, const qsc_model* m,
+                         int64_t* Y, void* stream);
+/* prob_probit: qmc/quantization_model.py:22-39, qmc/quantization_model_log.py:23-41.
+ * P = F(b[Y+1] - Xhat) - F(b[Y] - Xhat), F(y) = 0.5*(1 + erf(y / fp32(sigma*1.414213))). */
+QSC_API int qsc_prob_probit(const int64_t* Y, const float* Xhat, int64_t n, const qsc_model* m,
+                            float* P, void* stream);
+/* vector-Jacobian product of prob_probit w.r.t. Xhat: gX = gP * dP/dXhat */
+QSC_API int qsc_prob_probit_bwd(const int64_t* Y, const float* Xhat, const float* gP, int64_t n,
+                                const qsc_model* m, float* gX, void* stream);
+/* F_probit: qmc/quantization_model.py:57-61 */
+QSC_API int qsc_f_probit(const float* y, int64_t n, double sigma, float* out, void* stream);
+/* mid-bin values: get_quantized_obs_from_ordinal, qmc/quantization_model_log.py:43-51 */
+QSC_API int qsc_obs_from_ordinal(const int64_t* Y, int64_t n, const qsc_model* m, float* out,
+                                 void* stream);
+/* fold the Bernoulli sampling mask Wx (qmc/qmc.ipynb :493) into uint8 codes:
+ * codes = (Wx == 0) ? 0xFF : Y.  Wx may be NULL (all observed).  Entries with Y outside
+ * [0, nbins) are counted into *bad (device int32, caller zeroes it). */
+QSC_API int qsc_pack_codes(const int64_t* Y, const float* Wx, int64_t n, int32_t nbins,
+                           uint8_t* codes, int32_t* bad, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * reconstruction T = sum_r S_r (x) c_r
+ *   reference: outer qmc/quantization_model.py:70-77, get_tensor :79-86
+ *   (qmc/quantization_model_log.py:80-96).  The r-sum is accumulated in the reference's
+ *   order with separate fp32 multiply and add, so T is bit-identical to get_tensor.
+ * ------------------------------------------------------------------------------------- */
+QSC_API int qsc_reconstruct(const float* S, const float* C, int32_t R, int32_t P, int32_t K,
+                            float* T, void* stream);
+/* backward of get_tensor: dS[r][p] = sum_k gT[k][p] C[r][k], dC[r][k] = sum_p gT[k][p] S[r][p].
+ * Either output may be NULL.  Deterministic (fixed-order partial sums in ws). */
+QSC_API size_t qsc_reconstruct_bwd_workspace_bytes(int32_t R, int32_t P, int32_t K);
+QSC_API int qsc_reconstruct_bwd(const float* gT, const float* S, const float* C, int32_t R,
+                                int32_t P, int32_t K, float* dS, float* dC, void* ws,
+                                size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * reductions: NMSE qmc/quantization_model.py:88-92, NMSE_LOG qmc/quantization_model_log.py:104-111
+ * out2[0] = sum (f(a) - f(b))^2, out2[1] = sum f(b)^2 (fp64, device), f = identity or
+ * log(. + fp32(offset)) when use_log.  a == NULL means a = reconstruct(S, C) computed on the fly
+ * (fused: the map is never materialised).
+ * ------------------------------------------------------------------------------------- */
+QSC_API size_t qsc_reduce_workspace_bytes(int64_t n);
+QSC_API int qsc_diff_sumsq(const float* a, const float* b, int64_t n, int32_t use_log,
+                           double offset, double* out2, void* ws, size_t ws_bytes, void* stream);
+QSC_API int qsc_map_diff_sumsq(const float* S, const float* C, const float* Ttrue, int32_t R,
+                               int32_t P, int32_t K, int32_t use_log, double offset,
+                               double* out2, void* ws, size_t ws_bytes, void* stream);
+/* out[0] = sum x^2 (fp32 result, fixed order) */
+QSC_API int qsc_sumsq(const float* x, int64_t n, float* out, void* ws, size_t ws_bytes,
+                      void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * observation packing (one-time setup of a solve): dense codes -> sliced sparse formats.
+ * The reference evaluates every (k,p) entry and multiplies unobserved ones by Wx = 0
+ * (qmc/qmc.ipynb :572); the build reads only observed entries.
+ * ------------------------------------------------------------------------------------- */
+/* cnt[p] = number of observed k for pixel p (async) */
+QSC_API int qsc_obs_count(const uint8_t* codes, int32_t K, int32_t P, int32_t* cnt, void* stream);
+/* perm[q] = pixels sorted by cnt descending, stable; positions q >= P are padding (-1). */
+QSC_API size_t qsc_obs_order_workspace_bytes(int32_t P);
+QSC_API int qsc_obs_order(const int32_t* cnt, int32_t P, int32_t* perm, void* ws,
+                          size_t ws_bytes, void* stream);
+/* SYNCHRONOUS: computes slice widths/offsets of both formats and fills *desc.
+ * s_width[Pp/64], s_off[Pp/64 + 1], c_width[ntiles*nks], c_off[ntiles*nks + 1]. */
+QSC_API size_t qsc_obs_layout_workspace_bytes(int32_t K, int32_t P, int32_t PT);
+QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t PT, int32_t nbins,
+                           const int32_t* perm, const int32_t* cnt, int32_t* s_width,
+                           int64_t* s_off, int32_t* c_width, int64_t* c_off, void* ws,
+                           size_t ws_bytes, qsc_obs_desc* desc, void* stream);
+QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* desc, const int32_t* perm,
+                         const int32_t* s_width, const int64_t* s_off, const int32_t* c_width,
+                         const int64_t* c_off, void* s_entries, void* c_entries, void* stream);
+/* gather/scatter between natural pixel order [R][P] and position order [R][Pp] */
+QSC_API int qsc_perm_gather(const float* nat, const int32_t* perm, int32_t R, int32_t P,
+                            int32_t Pp, float* pos, void* stream);
+QSC_API int qsc_perm_scatter(const float* pos, const int32_t* perm, int32_t R, int32_t P,
+                             int32_t Pp, float* nat, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * fused likelihood + gradient passes (the hot path)
+ *   per observed entry e=(k,p):  t = sum_r S[r,p] C[r,k]  (reference order),
+ *   x = t (linear) or log(t + offset), P = prob_probit, nll -= log P,
+ *   g = (exp(-u^2) - exp(-w^2)) / (a sqrt(pi) P) * (log ? 1/(t+offset) : 1)
+ *   dS[r,p] = sum_k g C[r,k], dC[r,k] = sum_p g S[r,p]
+ *   (replaces get_tensor -> log -> prob_probit -> -sum(Wx log P) -> autograd backward,
+ *    qmc/qmc.ipynb :566-575 and :626-633)
+ * S, mS, vS, dS are in position order [R][Pp]; C, mC, vC in [R][K].
+ * ------------------------------------------------------------------------------------- */
+QSC_API size_t qsc_pass_workspace_bytes(const qsc_obs_desc* d, int32_t R);
+QSC_API int qsc_state_init(qsc_state* st, const float* S, int32_t R, int32_t Pp, void* ws,
+                           size_t ws_bytes, void* stream);
+/* S-pass.  mode 0: write dS (NLL gradient only, no regulariser) — used by the generator/DIP
+ * solvers and K-slab sharding; mode 1: fused S-step — dS + lambda_s*S/||S|| then Adam on S
+ * (S, mS, vS updated in place).  Writes per-block partials into ws. */
+QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
+                      const int64_t* s_off, const qsc_model* m, int32_t R, float* S,
+                      const float* C, int32_t mode, float* dS, float* mS, float* vS,
+                      const qsc_adam* adam, float lambda_s, qsc_state* st, void* ws,
+                      size_t ws_bytes, void* stream);
+/* C-pass: per-tile partial dC slab + NLL partials into ws. */
+QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_t* c_width,
+                      const int64_t* c_off, const qsc_model* m, int32_t R, const float* S,
+                      const float* C, void* ws, size_t ws_bytes, void* stream);
+/* reduce the C-pass slab.  mode 0: write dC (NLL gradient only); mode 1: fused C-step:
+ * dC + lambda_c*C/||C||, Adam on C, projection; also records st->nll_c, st->normsq_c.
+ * normsq_c_ext (device, nullable): global ||C||^2 supplied by the caller (K-slab sharding). */
+QSC_API int qsc_cfinish(const qsc_obs_desc* d, int32_t R, float* C, int32_t mode, float* dC,
+                        float* mC, float* vC, const qsc_adam* adam, float lambda_c,
+                        const float* normsq_c_ext, qsc_state* st, void* ws, size_t ws_bytes,
+                        void* stream);
+/* reduce the S-pass partials into st (nll_s, normsq_s of the updated S), advance counters,
+ * append [nll_c, nll_s, normsq_c, normsq_s] to hist[4*iter] (hist nullable). */
+QSC_API int qsc_sfinish(const qsc_obs_desc* d, int32_t R, qsc_state* st, float* hist,
+                        int32_t hist_cap, void* ws, size_t ws_bytes, void* stream);
+/* as qsc_sfinish with explicit flags: update_normsq (S was updated by the fused S-step),
+ * c_stepped / s_stepped (advance the Adam step counters of C / S). */
+QSC_API int qsc_sfinish_ex(const qsc_obs_desc* d, int32_t R, qsc_state* st, float* hist,
+                           int32_t hist_cap, int32_t update_normsq, int32_t c_stepped,
+                           int32_t s_stepped, void* ws, size_t ws_bytes, void* stream);
+/* plain Adam (torch.optim.Adam single-tensor semantics) with optional regulariser
+ * g += lambda * x / sqrt(*normsq) and projection; step counter taken from *step (+1, read
+ * only).  Used after an all-reduce of dS (K-slab sharding). */
+QSC_API int qsc_adam_step(float* x, float* mx, float* vx, const float* g, int64_t n,
+                          const qsc_adam* adam, const int32_t* step, float lambda,
+                          const float* normsq, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * R x R normal equations (MFMA): backup/algorithms/NMF_SPA.m:18-19 pseudo-inverse and
+ * backup/algorithms/joint_opt_ae.m:404-416 regularised least squares.
+ *   G[R][R] = sum_p w[p] S[r,p] S[r',p]      (w = pixel mask or NULL)     -- v_mfma_f32_16x16x4_f32
+ *   B[R][K] = sum_p w[p] S[r,p] T[k,p]
+ *   C = (G + lambda I)^-1 B                   (Cholesky, one workgroup)
+ * ------------------------------------------------------------------------------------- */
+QSC_API size_t qsc_gram_workspace_bytes(int32_t R, int32_t P, int32_t K);
+QSC_API int qsc_gram(const float* S, const float* w, int32_t R, int32_t P, float* G, void* ws,
+                     size_t ws_bytes, void* stream);
+QSC_API int qsc_gram_rhs(const float* S, const float* T, const float* w, int32_t R, int32_t P,
+                         int32_t K, float* B, void* ws, size_t ws_bytes, void* stream);
+QSC_API int qsc_chol_solve(const float* G, const float* B, int32_t R, int32_t K, float lambda,
+                           float* X, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QSC_H_ */

@@ -1,0 +1,55 @@
+"""ORACLE (test infrastructure only) — closed-form likelihood gradients in numpy fp64.
+
+Documents the math the fused HIP passes implement (include/qsc.h) and checks it against the
+reference's autograd (reference_ops.masked_nll + backward) to 1e-6.  For every observed entry
+e = (k, p) (Wx = 1; qmc/qmc.ipynb :493, :572):
+    t = sum_r S[r,p] C[r,k];  x = t  or  log(t + offset)
+    a = std * 1.414213;  u = (b[y+1] - x)/a;  w = (b[y] - x)/a       (linear: b[0]=-1e5, b[-1]=1e5)
+    P = 0.5 (1 + erf u) - 0.5 (1 + erf w);  nll = -sum log P
+    g = (exp(-u^2) - exp(-w^2)) / (a sqrt(pi) P) * (1/(t + offset) if log else 1)
+    dS[r,p] = sum_k g C[r,k];  dC[r,k] = sum_p g S[r,p]
+"""
+import math
+
+import numpy as np
+from scipy.special import erf
+
+
+def edges_of(b, log_model):
+    e = np.asarray(b, dtype=np.float64).copy()
+    if not log_model:
+        e[0], e[-1] = -1e5, 1e5
+    return e
+
+
+def nll_grad(S, C, Y, Wx, b, sigma, offset=0.0, log_model=False):
+    """S (R,P), C (R,K), Y (K,P) int, Wx (K,P) 0/1 -> (nll, dS (R,P), dC (R,K)) in fp64."""
+    S = np.asarray(S, np.float64)
+    C = np.asarray(C, np.float64)
+    Y = np.asarray(Y).astype(np.int64)
+    Wx = np.asarray(Wx, np.float64)
+    e = edges_of(b, log_model)
+    T = C.T @ S  # (K, P)
+    x = np.log(T + offset) if log_model else T
+    a = sigma * 1.414213
+    u = (e[Y + 1] - x) / a
+    w = (e[Y] - x) / a
+    P = 0.5 * (1 + erf(u)) - 0.5 * (1 + erf(w))
+    obs = Wx != 0
+    with np.errstate(divide="ignore", invalid="ignore"):
+        nll = -np.sum(np.log(P[obs]))
+        gx = (np.exp(-u * u) - np.exp(-w * w)) / (a * math.sqrt(math.pi) * P)
+    g = np.where(obs, gx * (1.0 / (T + offset) if log_model else 1.0), 0.0)
+    dS = C @ g          # (R,K)@(K,P)
+    dC = S @ g.T        # (R,P)@(P,K)
+    return nll, dS, dC
+
+
+def adam_step(p, m, v, g, step, lr, beta1=0.9, beta2=0.999, eps=1e-8):
+    """torch.optim.Adam single-tensor update in fp64 (reference for the fused epilogues)."""
+    m = beta1 * m + (1 - beta1) * g
+    v = beta2 * v + (1 - beta2) * g * g
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    p = p - (lr / bc1) * m / (np.sqrt(v) / math.sqrt(bc2) + eps)
+    return p, m, v

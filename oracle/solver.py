@@ -1,0 +1,49 @@
+"""ORACLE (test infrastructure only) — the alternating solver in the reference formulation.
+
+Re-enacts qmc/qmc.ipynb cell 1, loop :559-634 (C-step :562-579, S-step :622-634) with S as
+the free Adam variable (backup/notebooks/onebit_lowrank.ipynb:1230-1236): reference-style
+get_tensor (slice-assignment loop + autograd), prob_probit, the masked -sum(Wx log P),
+lambda_c ||C||_F + lambda_s ||S||_F, torch.optim.Adam and C[C<0] = 0.  This is also the CPU
+baseline bench.py times ("port"): the same op sequence, hence the same O(R K^2 I J) autograd
+cost as the reference.
+"""
+import time
+
+import torch
+
+from . import reference_ops as ro
+
+
+def free_s_solve(S0, C0, Y, Wx, b, sigma, offset=0.0, log_model=False, n_iter=10,
+                 lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2, snapshots=(), timer=None):
+    S = S0.clone().requires_grad_(True)
+    C = C0.clone().requires_grad_(True)
+    optC = torch.optim.Adam([C], lr=lr_c)
+    optS = torch.optim.Adam([S], lr=lr_s)
+    costs_c, costs_s, snaps, step_times = [], [], {}, []
+    for i in range(n_iter):
+        t0 = time.perf_counter()
+        Sc = S.detach().clone()
+        optC.zero_grad()
+        nll = ro.masked_nll(Sc, C, Y, Wx, b, sigma, offset, log_model)
+        cost = nll + lambda_c * torch.norm(C, "fro") + lambda_s * torch.norm(Sc, "fro")
+        cost.backward()
+        optC.step()
+        with torch.no_grad():
+            C[C < 0] = 0
+        costs_c.append(cost.item())
+        t1 = time.perf_counter()
+        optS.zero_grad()
+        nll = ro.masked_nll(S, C, Y, Wx, b, sigma, offset, log_model)
+        cost = nll + lambda_c * torch.norm(C, "fro") + lambda_s * torch.norm(S, "fro")
+        cost.backward()
+        optS.step()
+        costs_s.append(cost.item())
+        t2 = time.perf_counter()
+        step_times.append((t1 - t0, t2 - t1))
+        if i + 1 in snapshots:
+            snaps[i + 1] = (S.detach().clone(), C.detach().clone())
+        if timer is not None and timer(i + 1, t2 - t0):
+            break
+    return dict(S=S.detach(), C=C.detach(), costs_c=costs_c, costs_s=costs_s, snaps=snaps,
+                step_times=step_times)

@@ -1,0 +1,76 @@
+"""Build libqsc_hip.so (the gfx950 HIP kernels + C ABI) in-tree with hipcc.
+
+The shared library lands next to this file so that it travels with the repository snapshot
+to the GPU box (it is git-ignored, not gpurun-ignored).  No torch extension machinery is
+involved: the boundary is a plain C ABI (include/qsc.h) bound with ctypes.
+"""
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "libqsc_hip.so")
+SOURCES = ["qsc_ops.hip", "qsc_obs.hip", "qsc_pass.hip", "qsc_gram.hip"]
+ARCH = os.environ.get("QSC_OFFLOAD_ARCH", "gfx950")
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall",
+          "-Wno-unused-function"]
+
+
+def _hipcc():
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the HIP kernels of quantized_spectrum_cartography_amd "
+                       "need ROCm's hipcc to build")
+
+
+def _stale():
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+    deps.append(os.path.join(os.path.dirname(PKG_DIR), "include", "qsc.h"))
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force=False, verbose=True):
+    """Compile every HIP source for gfx950 and link libqsc_hip.so (parallel, one hipcc per file)."""
+    if not force and not _stale():
+        return LIB_PATH
+    hipcc = _hipcc()
+    tmp = tempfile.mkdtemp(prefix="qsc_build_")
+    try:
+        procs = []
+        objs = []
+        for src in SOURCES:
+            obj = os.path.join(tmp, src.replace(".hip", ".o"))
+            objs.append(obj)
+            cmd = [hipcc] + CFLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
+            procs.append((src, cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE,
+                                                     stderr=subprocess.STDOUT)))
+        failed = []
+        for src, cmd, p in procs:
+            out, _ = p.communicate()
+            if p.returncode != 0:
+                failed.append((src, out.decode(errors="replace")))
+            elif verbose and out:
+                sys.stderr.write(out.decode(errors="replace"))
+        if failed:
+            msg = "\n".join("---- %s ----\n%s" % f for f in failed)
+            raise RuntimeError("hipcc failed:\n" + msg)
+        out_tmp = LIB_PATH + ".tmp"
+        cmd = [hipcc, "-shared", "-fPIC", "--offload-arch=" + ARCH] + objs + ["-o", out_tmp]
+        subprocess.check_call(cmd)
+        os.replace(out_tmp, LIB_PATH)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    if verbose:
+        print("built", LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

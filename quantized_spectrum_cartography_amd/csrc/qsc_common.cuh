@@ -1,0 +1,198 @@
+// qsc_common.cuh — device helpers shared by the gfx950 kernels of libqsc_hip.so.
+//
+// Numerics follow the reference's torch CPU expressions op for op where that is cheap:
+//   F_probit(y, std) = (1/2)*(1 + erf(y/(std*1.414213)))      qmc/quantization_model.py:57-61
+//   the tensor / python-float division is a true fp32 division by fp32(std*1.414213)
+//   (measured on torch 2.10: 100 % match with correctly rounded x/a), reproduced here by a
+//   Markstein-corrected reciprocal multiply.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/qsc.h"
+
+#define QSC_WAVE 64
+
+#define QSC_CHECK_LAUNCH()                          \
+  do {                                              \
+    hipError_t e__ = hipGetLastError();             \
+    if (e__ != hipSuccess) return (int)e__;         \
+  } while (0)
+
+#define QSC_TRY(x)                                  \
+  do {                                              \
+    hipError_t e__ = (x);                           \
+    if (e__ != hipSuccess) return (int)e__;         \
+  } while (0)
+
+namespace qsc {
+
+// Derived per-call constants of the probit model, passed by value to kernels.
+struct Probit {
+  float a;        // fp32(sigma * 1.414213)
+  float inv_a;    // RN(1 / a)
+  float kgrad;    // 1 / (a * sqrt(pi))      d/dy F(y) = exp(-(y/a)^2) * kgrad
+  float offset;   // fp32(offset)
+  int log_model;
+  int nbins;
+  int lo_sat;     // linear model: erf((-1e5 - x)/a) == -1 exactly for every finite x of interest
+  int hi_sat;     // linear model: erf(( 1e5 - x)/a) ==  1
+};
+
+// host-side helper: build Probit from the C-ABI model
+inline Probit make_probit(const qsc_model* m) {
+  Probit p;
+  p.a = (float)(m->sigma * 1.414213);
+  p.inv_a = 1.0f / p.a;
+  p.kgrad = (float)(1.0 / ((double)p.a * 1.7724538509055160273));
+  p.offset = (float)m->offset;
+  p.log_model = m->log_model;
+  p.nbins = m->nbounds - 1;
+  // erf saturates to exactly +-1 in fp32 for |z| >= 3.92; the clamp edges are +-1e5.  The
+  // "saturated edge" shortcut is exact whenever 1e5/a stays far beyond that (a < 2.5e4).
+  int sat = (m->log_model == 0) && (p.a < 2.5e4f);
+  p.lo_sat = sat;
+  p.hi_sat = sat;
+  return p;
+}
+
+// Bin edge table: lo/hi boundary of code c (linear model clamps b[0], b[-1] to -/+1e5 as in
+// qmc/quantization_model.py:31-33; the log model uses the raw edges, _log.py:32-36).
+struct Edges {
+  float2 e[QSC_MAX_BOUNDS - 1];
+};
+
+inline void make_edges(const qsc_model* m, Edges* E) {
+  const int nb = m->nbounds;
+  for (int c = 0; c < nb - 1; ++c) {
+    float lo = m->bounds[c], hi = m->bounds[c + 1];
+    if (m->log_model == 0) {
+      if (c == 0) lo = -100000.0f;
+      if (c == nb - 2) hi = 100000.0f;
+    }
+    E->e[c] = make_float2(lo, hi);
+  }
+}
+
+// Correctly rounded x / a for a > 0 (one reciprocal multiply + one FMA residual correction).
+__device__ __forceinline__ float div_a(float x, const Probit& pr) {
+  float q = x * pr.inv_a;
+  float r = __builtin_fmaf(-q, pr.a, x);
+  return __builtin_fmaf(r, pr.inv_a, q);
+}
+
+// F_probit of an already-scaled argument z = y/a:  0.5f * (1.0f + erff(z))
+__device__ __forceinline__ float phi_scaled(float z) { return 0.5f * (1.0f + erff(z)); }
+
+// Likelihood of one observed entry with value x (already in the model domain) and code bin
+// edges (lo, hi):  P = F(hi - x) - F(lo - x),  gx = d(-log P)/dx.
+// `sat` selects the single-erf form for edges that saturate exactly (see make_probit).
+__device__ __forceinline__ void probit_lik(float x, float lo, float hi, bool lo_is_sat,
+                                           bool hi_is_sat, const Probit& pr, float& P,
+                                           float& gx) {
+  if (lo_is_sat) {
+    // F(lo - x) == 0.5f*(1 + (-1)) == 0 exactly
+    const float u = div_a(hi - x, pr);
+    P = phi_scaled(u);
+    gx = __expf(-u * u) * pr.kgrad / P;
+  } else if (hi_is_sat) {
+    // F(hi - x) == 0.5f*(1 + 1) == 1 exactly
+    const float w = div_a(lo - x, pr);
+    P = 1.0f - phi_scaled(w);
+    gx = -__expf(-w * w) * pr.kgrad / P;
+  } else {
+    const float u = div_a(hi - x, pr);
+    const float w = div_a(lo - x, pr);
+    P = phi_scaled(u) - phi_scaled(w);
+    gx = (__expf(-u * u) - __expf(-w * w)) * pr.kgrad / P;
+  }
+}
+
+// One observed entry end to end: t is the linear reconstruction value; returns P and the
+// gradient of -log P w.r.t. t (chain rule through log(t + offset) in the log model).
+__device__ __forceinline__ void entry_grad(float t, int code, const float2* edges,
+                                           const Probit& pr, float& P, float& g) {
+  float x = t, tinv = 1.0f;
+  if (pr.log_model) {
+    const float tp = t + pr.offset;
+    x = logf(tp);
+    tinv = 1.0f / tp;
+  }
+  const float2 e = edges[code];
+  const bool lo_sat = pr.lo_sat && code == 0;
+  const bool hi_sat = pr.hi_sat && code == pr.nbins - 1 && !lo_sat;
+  float gx;
+  probit_lik(x, e.x, e.y, lo_sat, hi_sat, pr, P, gx);
+  g = gx * tinv;
+}
+
+// ------------------------------------------------------------------------------------
+// reductions
+// ------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block sum in a fixed order (deterministic).  `sh` must hold blockDim.x/64 elements.
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* sh) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  T r = 0;
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int i = 0; i < nw; ++i) r += sh[i];
+  }
+  return r;  // valid in thread 0
+}
+
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+__host__ __device__ inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
+
+// Adam bias corrections exactly as torch.optim.Adam (_single_tensor_adam) forms them in
+// Python double precision, then hands them to fp32 tensor-scalar ops.
+struct AdamScalars {
+  float step_size;  // fp32(lr / (1 - beta1^step))
+  float bc2_sqrt;   // fp32(sqrt(1 - beta2^step))
+  float w1;         // fp32(1 - beta1)  (lerp weight)
+  float w2;         // fp32(1 - beta2)  (addcmul value)
+  float beta2;      // fp32(beta2)      (mul_ scalar)
+  float eps;        // fp32(eps)        (add_ scalar)
+};
+
+__device__ __forceinline__ AdamScalars adam_scalars(const qsc_adam& ad, int step) {
+  AdamScalars s;
+  const double b1 = ad.beta1, b2 = ad.beta2;
+  const double bc1 = 1.0 - pow(b1, (double)step);
+  const double bc2 = 1.0 - pow(b2, (double)step);
+  s.step_size = (float)(ad.lr / bc1);
+  s.beta2 = (float)b2;
+  s.eps = (float)ad.eps;
+  s.bc2_sqrt = (float)sqrt(bc2);
+  s.w1 = (float)(1.0 - b1);
+  s.w2 = (float)(1.0 - b2);
+  return s;
+}
+
+// One Adam element update (torch 2.x single-tensor path):
+//   m.lerp_(g, 1-b1)                        -> fma(w1, g - m, m)        (ATen's vectorised lerp)
+//   v.mul_(b2).addcmul_(g, g, value=1-b2)   -> fma(w2*g, g, v*b2)
+//   denom = v.sqrt() / bc2_sqrt + eps ;  p.addcdiv_(m, denom, value=-step_size) -> p + (-s*m)/denom
+// (each form checked bit-for-bit against torch 2.10 CPU on 2^20 random elements)
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
+                                          const qsc_adam& ad, const AdamScalars& s) {
+  m = __builtin_fmaf(s.w1, g - m, m);
+  const float vb = __fmul_rn(v, s.beta2);
+  v = __builtin_fmaf(__fmul_rn(s.w2, g), g, vb);
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), s.bc2_sqrt), s.eps);
+  p = __fadd_rn(p, __fdiv_rn(__fmul_rn(-s.step_size, m), denom));
+  if (ad.project_nonneg && p < 0.0f) p = 0.0f;
+}
+
+}  // namespace qsc

@@ -1,0 +1,318 @@
+// qsc_obs.hip — one-time packing of the observation tensor into the two sliced sparse formats
+// read by the fused passes (layout documented in include/qsc.h, qsc_obs_desc).
+//
+// Why: the reference evaluates the likelihood on every (k, p) entry and multiplies the
+// unobserved ones by Wx = 0 (qmc/qmc.ipynb :572, Wx ~ Bernoulli(f) per entry at :493).  At
+// f = 0.1 that is 90 % wasted arithmetic and, on a 64-lane wavefront, 64-way divergence.  The
+// passes instead walk only observed entries, one lane per pixel (S-pass) or per frequency bin
+// (C-pass), so every gradient sum stays in registers.  Pixels are re-ordered by observation
+// count (stable sort) so the 64 lanes of a slice carry near-equal work.
+#include <hipcub/hipcub.hpp>
+
+#include "qsc_common.cuh"
+
+using namespace qsc;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__global__ void __launch_bounds__(kBlock) count_kernel(const uint8_t* __restrict__ codes, int K,
+                                                       int P, int* __restrict__ cnt) {
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  int c = 0;
+  for (int k = 0; k < K; ++k) c += codes[(int64_t)k * P + p] != QSC_UNOBSERVED;
+  cnt[p] = c;
+}
+
+__global__ void iota_kernel(int* __restrict__ v, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = i;
+}
+
+__global__ void fill_int_kernel(int* __restrict__ v, int n, int val) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = val;
+}
+
+// S-format slice widths: 64 * round4(max count in the slice)
+__global__ void __launch_bounds__(kBlock) s_width_kernel(const int* __restrict__ perm,
+                                                         const int* __restrict__ cnt, int P,
+                                                         int nslices, int* __restrict__ width,
+                                                         int64_t* __restrict__ sizes) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nslices) return;
+  int m = 0;
+  for (int l = 0; l < 64; ++l) {
+    const int p = perm[s * 64 + l];
+    if (p >= 0 && p < P) m = max(m, cnt[p]);
+  }
+  m = (m + 3) & ~3;
+  width[s] = m;
+  sizes[s] = (int64_t)m * 64;
+}
+
+// C-format per (tile, k) counts via LDS integer atomics (order-independent), then widths.
+__global__ void __launch_bounds__(kBlock) c_width_kernel(const uint8_t* __restrict__ codes,
+                                                         const int* __restrict__ perm, int K,
+                                                         int P, int PT, int nks,
+                                                         int* __restrict__ width,
+                                                         int64_t* __restrict__ sizes) {
+  extern __shared__ int lcnt[];  // [nks*64]
+  const int t = blockIdx.x;
+  for (int i = threadIdx.x; i < nks * 64; i += blockDim.x) lcnt[i] = 0;
+  __syncthreads();
+  for (int ql = threadIdx.x; ql < PT; ql += blockDim.x) {
+    const int p = perm[(int64_t)t * PT + ql];
+    if (p < 0 || p >= P) continue;
+    for (int k = 0; k < K; ++k)
+      if (codes[(int64_t)k * P + p] != QSC_UNOBSERVED) atomicAdd(&lcnt[k], 1);
+  }
+  __syncthreads();
+  for (int ks = threadIdx.x; ks < nks; ks += blockDim.x) {
+    int m = 0;
+    for (int l = 0; l < 64; ++l) m = max(m, lcnt[ks * 64 + l]);
+    m = (m + 3) & ~3;
+    width[(int64_t)t * nks + ks] = m;
+    sizes[(int64_t)t * nks + ks] = (int64_t)m * 64;
+  }
+}
+
+template <typename E>
+struct EntryTraits;
+template <>
+struct EntryTraits<uint16_t> {
+  static constexpr int kBits = 12;
+  static constexpr uint32_t kPad = 15;
+};
+template <>
+struct EntryTraits<uint32_t> {
+  static constexpr int kBits = 24;
+  static constexpr uint32_t kPad = 255;
+};
+
+__device__ __forceinline__ int64_t slot(int64_t base, int lane, int j) {
+  return base + (int64_t)(j >> 2) * 256 + lane * 4 + (j & 3);
+}
+
+template <typename E>
+__global__ void __launch_bounds__(kBlock) s_fill_kernel(const uint8_t* __restrict__ codes,
+                                                        const int* __restrict__ perm, int K,
+                                                        int P, int Pp,
+                                                        const int* __restrict__ width,
+                                                        const int64_t* __restrict__ off,
+                                                        E* __restrict__ ent) {
+  using Tr = EntryTraits<E>;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Pp) return;
+  const int s = q >> 6, lane = q & 63;
+  const int W = width[s];
+  const int64_t base = off[s];
+  const int p = perm[q];
+  int j = 0;
+  if (p >= 0 && p < P) {
+    for (int k = 0; k < K; ++k) {
+      const uint8_t c = codes[(int64_t)k * P + p];
+      if (c != QSC_UNOBSERVED) ent[slot(base, lane, j++)] = (E)((uint32_t)k | ((uint32_t)c << Tr::kBits));
+    }
+  }
+  for (; j < W; ++j) ent[slot(base, lane, j)] = (E)(Tr::kPad << Tr::kBits);
+}
+
+template <typename E>
+__global__ void __launch_bounds__(kBlock) c_fill_kernel(const uint8_t* __restrict__ codes,
+                                                        const int* __restrict__ perm, int K,
+                                                        int P, int PT, int nks,
+                                                        const int* __restrict__ width,
+                                                        const int64_t* __restrict__ off,
+                                                        E* __restrict__ ent) {
+  using Tr = EntryTraits<E>;
+  const int t = blockIdx.x;
+  for (int kk = threadIdx.x; kk < nks * 64; kk += blockDim.x) {
+    const int ks = kk >> 6, lane = kk & 63;
+    const int64_t wi = (int64_t)t * nks + ks;
+    const int W = width[wi];
+    const int64_t base = off[wi];
+    int j = 0;
+    if (kk < K) {
+      for (int ql = 0; ql < PT; ++ql) {
+        const int p = perm[(int64_t)t * PT + ql];
+        if (p < 0 || p >= P) continue;
+        const uint8_t c = codes[(int64_t)kk * P + p];
+        if (c != QSC_UNOBSERVED) ent[slot(base, lane, j++)] = (E)((uint32_t)ql | ((uint32_t)c << Tr::kBits));
+      }
+    }
+    for (; j < W; ++j) ent[slot(base, lane, j)] = (E)(Tr::kPad << Tr::kBits);
+  }
+}
+
+struct LayoutWs {
+  int64_t* s_sizes;
+  int64_t* c_sizes;
+  int64_t* totals;  // [3]: s_entries, c_entries, nnz
+  void* cub;
+  size_t cub_bytes;
+};
+
+inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+size_t cub_scan_bytes(int n) {
+  size_t b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (int64_t*)nullptr, (int64_t*)nullptr, n);
+  return b;
+}
+size_t cub_reduce_bytes(int n) {
+  size_t b = 0;
+  (void)hipcub::DeviceReduce::Sum(nullptr, b, (int*)nullptr, (int64_t*)nullptr, n);
+  return b;
+}
+
+}  // namespace
+
+#define STREAM(s) reinterpret_cast<hipStream_t>(s)
+
+extern "C" {
+
+QSC_API int qsc_obs_count(const uint8_t* codes, int32_t K, int32_t P, int32_t* cnt, void* stream) {
+  if (K < 1 || P < 1 || !codes || !cnt) return QSC_EINVAL;
+  hipLaunchKernelGGL(count_kernel, dim3((unsigned)ceil_div(P, kBlock)), dim3(kBlock), 0,
+                     STREAM(stream), codes, K, P, cnt);
+  QSC_CHECK_LAUNCH();
+  return QSC_OK;
+}
+
+QSC_API size_t qsc_obs_order_workspace_bytes(int32_t P) {
+  size_t b = 0;
+  (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, b, (int*)nullptr, (int*)nullptr,
+                                               (int*)nullptr, (int*)nullptr, P);
+  return align_up(b) + 3 * align_up((size_t)P * sizeof(int));
+}
+
+QSC_API int qsc_obs_order(const int32_t* cnt, int32_t P, int32_t* perm, void* ws,
+                          size_t ws_bytes, void* stream) {
+  if (P < 1 || !cnt || !perm || !ws || ws_bytes < qsc_obs_order_workspace_bytes(P))
+    return QSC_EINVAL;
+  size_t cub_b = 0;
+  (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, cub_b, (int*)nullptr, (int*)nullptr,
+                                               (int*)nullptr, (int*)nullptr, P);
+  char* w = (char*)ws;
+  void* cub = w;
+  w += align_up(cub_b);
+  int* keys_out = (int*)w;
+  w += align_up((size_t)P * sizeof(int));
+  int* vals_in = (int*)w;
+  hipStream_t s = STREAM(stream);
+  hipLaunchKernelGGL(iota_kernel, dim3((unsigned)ceil_div(P, kBlock)), dim3(kBlock), 0, s, vals_in, P);
+  QSC_CHECK_LAUNCH();
+  hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(cub, cub_b, cnt, keys_out, vals_in,
+                                                              perm, P, 0, 32, s);
+  if (e != hipSuccess) return (int)e;
+  const int Pp = (int)round_up(P, 64);
+  if (Pp > P) {
+    hipLaunchKernelGGL(fill_int_kernel, dim3(1), dim3(64), 0, s, perm + P, Pp - P, -1);
+    QSC_CHECK_LAUNCH();
+  }
+  return QSC_OK;
+}
+
+QSC_API size_t qsc_obs_layout_workspace_bytes(int32_t K, int32_t P, int32_t PT) {
+  const int64_t Pp = round_up(P, 64);
+  const int64_t ns = Pp / 64;
+  const int64_t nt = ceil_div(Pp, PT > 0 ? PT : 64);
+  const int64_t nc = nt * ceil_div(K, 64);
+  size_t cb = cub_scan_bytes((int)(ns + 1));
+  cb = std::max(cb, cub_scan_bytes((int)(nc + 1)));
+  cb = std::max(cb, cub_reduce_bytes(P));
+  return align_up((ns + 1) * 8) + align_up((nc + 1) * 8) + align_up(3 * 8) + align_up(cb);
+}
+
+QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t PT, int32_t nbins,
+                           const int32_t* perm, const int32_t* cnt, int32_t* s_width,
+                           int64_t* s_off, int32_t* c_width, int64_t* c_off, void* ws,
+                           size_t ws_bytes, qsc_obs_desc* desc, void* stream) {
+  if (K < 1 || P < 1 || PT < 64 || (PT & 63) || nbins < 1 || nbins > QSC_MAX_BOUNDS - 1 ||
+      !codes || !perm || !cnt || !s_width || !s_off || !c_width || !c_off || !desc || !ws ||
+      ws_bytes < qsc_obs_layout_workspace_bytes(K, P, PT))
+    return QSC_EINVAL;
+  const int Pp = (int)round_up(P, 64);
+  if (Pp % PT) return QSC_EINVAL;
+  const int ns = Pp / 64, nt = Pp / PT, nks = (int)ceil_div(K, 64);
+  if ((int64_t)nks * 64 * sizeof(int) > 64 * 1024) return QSC_EINVAL;  // LDS counters
+  const int wide = (K > 4096 || PT > 4096 || nbins > 15) ? 1 : 0;
+  if (wide && ((int64_t)K >= (1 << 24) || (int64_t)PT >= (1 << 24))) return QSC_EINVAL;
+  char* w = (char*)ws;
+  int64_t* s_sizes = (int64_t*)w;
+  w += align_up((size_t)(ns + 1) * 8);
+  int64_t* c_sizes = (int64_t*)w;
+  w += align_up((size_t)(nt * nks + 1) * 8);
+  int64_t* totals = (int64_t*)w;
+  w += align_up(3 * 8);
+  void* cub = w;
+  size_t cub_b = ws_bytes - (size_t)(w - (char*)ws);
+  hipStream_t s = STREAM(stream);
+  hipLaunchKernelGGL(s_width_kernel, dim3((unsigned)ceil_div(ns, kBlock)), dim3(kBlock), 0, s,
+                     perm, cnt, P, ns, s_width, s_sizes);
+  QSC_CHECK_LAUNCH();
+  QSC_TRY(hipMemsetAsync(s_sizes + ns, 0, 8, s));
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(cub, cub_b, s_sizes, s_off, ns + 1, s);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(c_width_kernel, dim3((unsigned)nt), dim3(kBlock), nks * 64 * sizeof(int), s,
+                     codes, perm, K, P, PT, nks, c_width, c_sizes);
+  QSC_CHECK_LAUNCH();
+  QSC_TRY(hipMemsetAsync(c_sizes + (int64_t)nt * nks, 0, 8, s));
+  cub_b = ws_bytes - (size_t)((char*)cub - (char*)ws);
+  e = hipcub::DeviceScan::ExclusiveSum(cub, cub_b, c_sizes, c_off, nt * nks + 1, s);
+  if (e != hipSuccess) return (int)e;
+  cub_b = ws_bytes - (size_t)((char*)cub - (char*)ws);
+  e = hipcub::DeviceReduce::Sum(cub, cub_b, cnt, totals + 2, P, s);
+  if (e != hipSuccess) return (int)e;
+  QSC_TRY(hipMemcpyAsync(totals, s_off + ns, 8, hipMemcpyDeviceToDevice, s));
+  QSC_TRY(hipMemcpyAsync(totals + 1, c_off + (int64_t)nt * nks, 8, hipMemcpyDeviceToDevice, s));
+  int64_t host_tot[3];
+  e = hipMemcpyAsync(host_tot, totals, sizeof(host_tot), hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return (int)e;
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return (int)e;
+  desc->K = K;
+  desc->P = P;
+  desc->Pp = Pp;
+  desc->PT = PT;
+  desc->ntiles = nt;
+  desc->nks = nks;
+  desc->wide = wide;
+  desc->nbins = nbins;
+  desc->s_entries = host_tot[0];
+  desc->c_entries = host_tot[1];
+  desc->nnz = host_tot[2];
+  return QSC_OK;
+}
+
+QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* d, const int32_t* perm,
+                         const int32_t* s_width, const int64_t* s_off, const int32_t* c_width,
+                         const int64_t* c_off, void* s_entries, void* c_entries, void* stream) {
+  if (!d || !codes || !perm || !s_width || !s_off || !c_width || !c_off) return QSC_EINVAL;
+  if ((d->s_entries > 0 && !s_entries) || (d->c_entries > 0 && !c_entries)) return QSC_EINVAL;
+  hipStream_t s = STREAM(stream);
+  if (d->wide) {
+    hipLaunchKernelGGL(s_fill_kernel<uint32_t>, dim3((unsigned)ceil_div(d->Pp, kBlock)),
+                       dim3(kBlock), 0, s, codes, perm, d->K, d->P, d->Pp, s_width, s_off,
+                       (uint32_t*)s_entries);
+    QSC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(c_fill_kernel<uint32_t>, dim3((unsigned)d->ntiles), dim3(kBlock), 0, s,
+                       codes, perm, d->K, d->P, d->PT, d->nks, c_width, c_off,
+                       (uint32_t*)c_entries);
+  } else {
+    hipLaunchKernelGGL(s_fill_kernel<uint16_t>, dim3((unsigned)ceil_div(d->Pp, kBlock)),
+                       dim3(kBlock), 0, s, codes, perm, d->K, d->P, d->Pp, s_width, s_off,
+                       (uint16_t*)s_entries);
+    QSC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(c_fill_kernel<uint16_t>, dim3((unsigned)d->ntiles), dim3(kBlock), 0, s,
+                       codes, perm, d->K, d->P, d->PT, d->nks, c_width, c_off,
+                       (uint16_t*)c_entries);
+  }
+  QSC_CHECK_LAUNCH();
+  return QSC_OK;
+}
+
+}  // extern "C"

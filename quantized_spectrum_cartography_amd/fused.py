@@ -1,0 +1,119 @@
+"""Fused likelihood + gradient passes over packed observations (the hot path).
+
+One *grad-step*  is one pass plus the update of the block it
+differentiates:
+  C-step:  qsc_cpass (per-tile dC partials)  ->  qsc_cfinish (fixed-order reduction,
+           + lambda_c C/||C||, Adam, C[C<0] = 0)               qmc/qmc.ipynb :562-579
+  S-step:  qsc_spass (dS in registers, + lambda_s S/||S||, Adam fused in the epilogue)
+           ->  qsc_sfinish (scalars, step counters)             qmc/qmc.ipynb :622-634
+All scalars (step counters, ||S||^2, NLLs) stay on the device, so an iteration is four
+kernel launches with no host synchronisation and can be captured in one hipGraph.
+"""
+import torch
+
+from . import _lib
+from ._model import _dev, _ws
+
+
+class PassEngine:
+    """Workspace + device state for running the fused passes on one Observations set."""
+
+    def __init__(self, obs, R, hist_cap=0):
+        if not 1 <= R <= _lib.QSC_MAX_R:
+            raise ValueError("rank R must be in [1, %d]" % _lib.QSC_MAX_R)
+        self.obs, self.R = obs, R
+        dev = obs.device
+        nb = _lib.lib().qsc_pass_workspace_bytes(obs.desc, R)
+        if nb == 0:
+            raise _lib.QscError("invalid observation descriptor")
+        self.ws = _ws(nb, dev)
+        self.state = torch.zeros(_lib.STATE_BYTES, dtype=torch.uint8, device=dev)
+        self.hist_cap = int(hist_cap)
+        self.hist = torch.zeros(max(4 * self.hist_cap, 4), dtype=torch.float32, device=dev)
+
+    # ---- state --------------------------------------------------------------------------
+    def init_state(self, S_pos):
+        ws = _ws(256 * 8, S_pos.device)
+        _lib.call("qsc_state_init", _lib.ptr(self.state), _lib.ptr(S_pos), self.R, self.obs.Pp,
+                  _lib.ptr(ws), ws.numel(), _lib.stream())
+
+    def read_state(self):
+        return _lib.read_state(self.state)
+
+    # ---- passes -------------------------------------------------------------------------
+    def cpass(self, S_pos, C):
+        o = self.obs
+        _lib.call("qsc_cpass", o.desc, _lib.ptr(o.c_entries), _lib.ptr(o.c_width), _lib.ptr(o.c_off),
+                  o.model, self.R, _lib.ptr(S_pos), _lib.ptr(C), _lib.ptr(self.ws), self.ws.numel(),
+                  _lib.stream())
+
+    def cfinish(self, C, mode, dC=None, mC=None, vC=None, adam=None, lambda_c=0.0, normsq_ext=None):
+        _lib.call("qsc_cfinish", self.obs.desc, self.R, _lib.ptr(C), int(mode), _lib.ptr(dC),
+                  _lib.ptr(mC), _lib.ptr(vC), adam, float(lambda_c), _lib.ptr(normsq_ext),
+                  _lib.ptr(self.state), _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
+
+    def spass(self, S_pos, C, mode, dS=None, mS=None, vS=None, adam=None, lambda_s=0.0):
+        o = self.obs
+        _lib.call("qsc_spass", o.desc, _lib.ptr(o.s_entries), _lib.ptr(o.s_width), _lib.ptr(o.s_off),
+                  o.model, self.R, _lib.ptr(S_pos), _lib.ptr(C), int(mode), _lib.ptr(dS),
+                  _lib.ptr(mS), _lib.ptr(vS), adam, float(lambda_s), _lib.ptr(self.state),
+                  _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
+
+    def sfinish(self, update_normsq=True, c_stepped=True, s_stepped=True):
+        _lib.call("qsc_sfinish_ex", self.obs.desc, self.R, _lib.ptr(self.state), _lib.ptr(self.hist),
+                  self.hist_cap, int(update_normsq), int(c_stepped), int(s_stepped),
+                  _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
+
+    # ---- composite ----------------------------------------------------------------------
+    def nll_grad(self, S_pos, C, need_dS=True, need_dC=True):
+        """NLL (device scalar) and its gradients dS (position order) and dC, no regularisers."""
+        R, Pp = self.R, self.obs.Pp
+        dS = torch.empty((R, Pp), dtype=torch.float32, device=S_pos.device) if need_dS else None
+        dC = torch.empty_like(C) if need_dC else None
+        if need_dC:
+            self.cpass(S_pos, C)
+            self.cfinish(C, 0, dC=dC)
+        if need_dS:
+            self.spass(S_pos, C, 0, dS=dS)
+            self.sfinish(update_normsq=False, c_stepped=False, s_stepped=False)
+            nll = self.state[28:32].view(torch.float32)[0].clone()  # nll_s
+        else:
+            nll = self.state[24:28].view(torch.float32)[0].clone()  # nll_c
+        return nll, dS, dC
+
+
+class _ProbitNLLFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, S, C, obs):
+        R = S.shape[0]
+        eng = PassEngine(obs, R)
+        Cd = _dev(C.detach().to(torch.float32)).contiguous()
+        S_pos = obs.to_positions(S.detach().reshape(R, -1))
+        nll, dS_pos, dC = eng.nll_grad(S_pos, Cd, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        dS = obs.to_pixels(dS_pos).reshape(S.shape) if dS_pos is not None else None
+        ctx.save_for_backward(*(t for t in (dS, dC) if t is not None))
+        ctx.has = (dS is not None, dC is not None)
+        return nll
+
+    @staticmethod
+    def backward(ctx, g):
+        saved = list(ctx.saved_tensors)
+        dS = saved.pop(0) * g if ctx.has[0] else None
+        dC = saved.pop(0) * g if ctx.has[1] else None
+        return dS, dC, None
+
+
+class ProbitNLL:
+    """-sum(Wx * log(prob_probit(Y, T_hat, b, std))) with T_hat = get_tensor(S, C) (optionally
+    log(T_hat + offset)), evaluated by the fused HIP passes over observed entries only.
+
+    Replaces the reference's get_tensor -> log -> prob_probit -> log -> masked sum chain
+    (qmc/qmc.ipynb :568-572) and its autograd backward.  Usage:
+        nll = ProbitNLL.apply(S, C, obs); (nll + lam*torch.norm(C)).backward()
+    """
+
+    @staticmethod
+    def apply(S, C, obs):
+        if S.dim() == 3:
+            S = S.unsqueeze(1)
+        return _ProbitNLLFn.apply(S, C, obs)

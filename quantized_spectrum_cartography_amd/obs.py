@@ -1,0 +1,138 @@
+"""Observation sets: the quantized, sparsely sampled map packed for the fused HIP passes.
+
+The reference keeps the observation as a dense int64 tensor Y (K,1,I,J) plus a dense float
+mask Wx (qmc/qmc.ipynb :493, :537) and evaluates every entry.  `Observations` folds the mask
+into uint8 codes (0xFF = unobserved), then packs only the observed entries into the two
+sliced formats of include/qsc.h (one per pass), with pixels re-ordered by observation count
+so that the 64 lanes of every wavefront carry near-equal work.  Built once per solve.
+"""
+import torch
+
+from . import _lib
+from ._model import _dev, _ws
+
+
+def default_tile(P, R, K):
+    """C-pass pixel tile: ~512 tiles to fill 256 CUs, S tile in LDS <= 64 KB, <= 4096."""
+    Pp = -(-P // 64) * 64
+    rp = 4 if R <= 4 else (8 if R <= 8 else 16)
+    cap = min(4096, (64 * 1024) // (rp * 4))
+    cap -= cap % 64
+    want = max(64, -(-Pp // 512))
+    want = -(-want // 64) * 64
+    PT = min(want, cap)
+    # PT must divide Pp
+    while Pp % PT:
+        PT -= 64
+    return PT
+
+
+class Observations:
+    """Packed observations of one K-slab.
+
+    Args:
+      Y: bin indices, (K,1,I,J) or (K,I,J) integer tensor (quantize output).
+      Wx: sampling mask of the same shape (0/1 floats) or None (all observed).
+      bin_boundaries, noise_std, offset, log_model: the probit model (see quantization_model*).
+      perm: optional (Pp,) int32 pixel order shared across ranks (K-slab sharding).
+      tile: optional C-pass tile size (positions, multiple of 64).
+    """
+
+    def __init__(self, Y, Wx, bin_boundaries, noise_std, offset=0.0, log_model=False, perm=None,
+                 tile=None, R_hint=8):
+        K = Y.shape[0]
+        I, J = Y.shape[-2], Y.shape[-1]
+        P = I * J
+        self.K, self.I, self.J, self.P = K, I, J, P
+        self.Pp = -(-P // 64) * 64
+        self.model = _lib.make_model(bin_boundaries, noise_std, offset if log_model else 0.0,
+                                     log_model)
+        self.log_model = bool(log_model)
+        self.noise_std = float(noise_std)
+        self.offset = float(offset or 0.0)
+        self.bin_boundaries = [float(x) for x in (bin_boundaries.tolist() if isinstance(
+            bin_boundaries, torch.Tensor) else bin_boundaries)]
+        nbins = len(self.bin_boundaries) - 1
+        if nbins > 254:
+            raise ValueError("at most 254 bins are supported (code 0xFF marks unobserved)")
+        Yd = _dev(Y.reshape(K, P).to(torch.int64))
+        dev = Yd.device
+        self.device = dev
+        Wd = _dev(Wx.reshape(K, P).to(torch.float32)) if Wx is not None else None
+        codes = torch.empty((K, P), dtype=torch.uint8, device=dev)
+        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.call("qsc_pack_codes", _lib.ptr(Yd), _lib.ptr(Wd), K * P, nbins, _lib.ptr(codes),
+                  _lib.ptr(bad), _lib.stream())
+        nbad = int(bad.item())
+        if nbad:
+            raise ValueError("%d observed entries have a code outside [0, %d) or a sampling "
+                             "weight other than 0/1" % (nbad, nbins))
+        self.codes = codes
+        s = _lib.stream()
+        cnt = torch.empty(P, dtype=torch.int32, device=dev)
+        _lib.call("qsc_obs_count", _lib.ptr(codes), K, P, _lib.ptr(cnt), s)
+        self.counts = cnt
+        if perm is None:
+            perm = torch.empty(self.Pp, dtype=torch.int32, device=dev)
+            ws = _ws(_lib.lib().qsc_obs_order_workspace_bytes(P), dev)
+            _lib.call("qsc_obs_order", _lib.ptr(cnt), P, _lib.ptr(perm), _lib.ptr(ws), ws.numel(), s)
+        else:
+            perm = _dev(perm.to(torch.int32))
+            if perm.numel() != self.Pp:
+                raise ValueError("perm must have Pp = %d entries" % self.Pp)
+        self.perm = perm
+        PT = tile or default_tile(P, R_hint, K)
+        if PT % 64 or self.Pp % PT:
+            raise ValueError("tile must be a multiple of 64 dividing Pp=%d" % self.Pp)
+        ns, nt, nks = self.Pp // 64, self.Pp // PT, -(-K // 64)
+        self.s_width = torch.empty(ns, dtype=torch.int32, device=dev)
+        self.s_off = torch.empty(ns + 1, dtype=torch.int64, device=dev)
+        self.c_width = torch.empty(nt * nks, dtype=torch.int32, device=dev)
+        self.c_off = torch.empty(nt * nks + 1, dtype=torch.int64, device=dev)
+        desc = _lib.QscObsDesc()
+        ws = _ws(_lib.lib().qsc_obs_layout_workspace_bytes(K, P, PT), dev)
+        _lib.call("qsc_obs_layout", _lib.ptr(codes), K, P, PT, nbins, _lib.ptr(perm), _lib.ptr(cnt),
+                  _lib.ptr(self.s_width), _lib.ptr(self.s_off), _lib.ptr(self.c_width),
+                  _lib.ptr(self.c_off), _lib.ptr(ws), ws.numel(), desc, s)
+        self.desc = desc
+        et = torch.int32 if desc.wide else torch.int16
+        self.s_entries = torch.empty(max(desc.s_entries, 1), dtype=et, device=dev)
+        self.c_entries = torch.empty(max(desc.c_entries, 1), dtype=et, device=dev)
+        _lib.call("qsc_obs_fill", _lib.ptr(codes), desc, _lib.ptr(perm), _lib.ptr(self.s_width),
+                  _lib.ptr(self.s_off), _lib.ptr(self.c_width), _lib.ptr(self.c_off),
+                  _lib.ptr(self.s_entries), _lib.ptr(self.c_entries), s)
+
+    # ---- info -----------------------------------------------------------------------
+    @property
+    def nnz(self):
+        return int(self.desc.nnz)
+
+    @property
+    def entry_bytes(self):
+        return 4 if self.desc.wide else 2
+
+    def stats(self):
+        d = self.desc
+        return dict(K=d.K, P=d.P, Pp=d.Pp, tile=d.PT, ntiles=d.ntiles, nks=d.nks, wide=d.wide,
+                    nbins=d.nbins, nnz=d.nnz, s_entries=d.s_entries, c_entries=d.c_entries,
+                    s_padding=d.s_entries / max(d.nnz, 1) - 1.0,
+                    c_padding=d.c_entries / max(d.nnz, 1) - 1.0)
+
+    # ---- order conversions -------------------------------------------------------------
+    def to_positions(self, X):
+        """(R, P) natural pixel order -> (R, Pp) position order."""
+        R = X.shape[0]
+        Xd = _dev(X.detach().to(torch.float32)).reshape(R, self.P)
+        out = torch.empty((R, self.Pp), dtype=torch.float32, device=Xd.device)
+        _lib.call("qsc_perm_gather", _lib.ptr(Xd), _lib.ptr(self.perm), R, self.P, self.Pp,
+                  _lib.ptr(out), _lib.stream())
+        return out
+
+    def to_pixels(self, Xp, out=None):
+        """(R, Pp) position order -> (R, P) natural pixel order."""
+        R = Xp.shape[0]
+        if out is None:
+            out = torch.empty((R, self.P), dtype=torch.float32, device=Xp.device)
+        _lib.call("qsc_perm_scatter", _lib.ptr(Xp), _lib.ptr(self.perm), R, self.P, self.Pp,
+                  _lib.ptr(out), _lib.stream())
+        return out

@@ -1,0 +1,249 @@
+"""Alternating S/C maximum-likelihood solver — the drop-in for the qmc.py / qmc.ipynb solver.
+
+The reference's solver is the notebook cell qmc/qmc.ipynb cell 1 (raw-JSON lines :422-653,
+loop at :559-645); qmc/qmc.py is only its import preamble.  Per outer iteration it runs
+  C-step (cinnerIter = 1):  cost = -sum(Wx log P(Y | T_hat(S, C))) + lambda_c ||C||_F
+                            + lambda_s ||Z||_F;  Adam(lr 5e-3) on C;  C[C<0] = 0      (:562-579)
+  S-step (sinnerIter = 1):  same cost;  Adam(lr 1e-2) on Z with S = G(Z)            (:622-634)
+`solve` reproduces that loop in two modes:
+  * free S (generator=None): S itself is the Adam variable with lambda_s ||S||_F, the form of
+    backup/notebooks/onebit_lowrank.ipynb:1230-1236 (needed for maps that are not 51x51);
+    every grad-step is a fused HIP pass with the Adam update on the device, no host sync.
+  * generator (S = generator(Z)): the C-step is the fused HIP C-step; the S-step gets dS from
+    the fused HIP S-pass and back-propagates it through the torch generator to Z (the
+    reference's GAN path, Z optimised, network frozen: :547-550).
+"""
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+
+from . import _lib
+from ._model import _dev, map_nmse
+from .fused import PassEngine
+from .obs import Observations
+
+
+@dataclass
+class SolveResult:
+    S: torch.Tensor                     # (R, 1, I, J), natural pixel order
+    C: torch.Tensor                     # (R, K)
+    costs_c: List[float]                # cost evaluated in each C-step (before the update)
+    costs_s: List[float]                # cost evaluated in each S-step (before the update)
+    nmse: List[float] = field(default_factory=list)  # map NMSE after each tracked iteration
+    Z: Optional[torch.Tensor] = None
+    iters: int = 0
+
+
+class FreeSSolver:
+    """Device-resident free-S alternating solver over one Observations set.
+
+    State (position-ordered S, Adam moments, step counters, ||S||^2, NLLs) lives on the GPU.
+    `run(n)` issues 4 launches per iteration; with `use_graph` the iteration is captured once
+    in a hipGraph (torch.cuda.CUDAGraph) and replayed.
+    """
+
+    def __init__(self, obs, S_init, C_init, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
+                 betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024):
+        self.obs = obs
+        R = S_init.shape[0]
+        self.R = R
+        self.engine = PassEngine(obs, R, hist_cap=hist_cap)
+        self.S = obs.to_positions(S_init.reshape(R, -1))
+        self.C = _dev(C_init.detach().to(torch.float32)).reshape(R, obs.K).clone()
+        self.mS, self.vS = torch.zeros_like(self.S), torch.zeros_like(self.S)
+        self.mC, self.vC = torch.zeros_like(self.C), torch.zeros_like(self.C)
+        self.adam_c = _lib.make_adam(lr_c, betas, eps, project_nonneg=project_c)
+        self.adam_s = _lib.make_adam(lr_s, betas, eps, project_nonneg=False)
+        self.lambda_c, self.lambda_s = float(lambda_c), float(lambda_s)
+        self.engine.init_state(self.S)
+        self._graph = None
+        self._graph_iters = 0
+
+    # one outer iteration = C grad-step + S grad-step
+    def c_step(self):
+        e = self.engine
+        e.cpass(self.S, self.C)
+        e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)
+
+    def s_step(self):
+        e = self.engine
+        e.spass(self.S, self.C, 1, mS=self.mS, vS=self.vS, adam=self.adam_s, lambda_s=self.lambda_s)
+        e.sfinish(update_normsq=True, c_stepped=True, s_stepped=True)
+
+    def iteration(self):
+        self.c_step()
+        self.s_step()
+
+    def capture(self, iters=1):
+        """Capture `iters` iterations into one graph (replayed by run)."""
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(iters):
+                    self.iteration()
+        torch.cuda.current_stream().wait_stream(s)
+        self._graph, self._graph_iters = g, iters
+
+    def run(self, n, use_graph=False):
+        if use_graph:
+            if self._graph is None:
+                self.capture(1 if n < 8 else 8)
+            k = n // self._graph_iters
+            for _ in range(k):
+                self._graph.replay()
+            for _ in range(n - k * self._graph_iters):
+                self.iteration()
+        else:
+            for _ in range(n):
+                self.iteration()
+
+    # ---- results --------------------------------------------------------------------------
+    def state(self):
+        return self.engine.read_state()
+
+    def S_pixels(self):
+        return self.obs.to_pixels(self.S).reshape(self.R, 1, self.obs.I, self.obs.J)
+
+    def history(self):
+        st = self.state()
+        n = min(int(st["iter"]), self.engine.hist_cap)
+        h = self.engine.hist[: 4 * n].view(n, 4).double().cpu()
+        nsq_c_final = float((self.C.double() ** 2).sum().item())
+        costs_c, costs_s = [], []
+        for i in range(n):
+            nll_c, nll_s, nsq_c, nsq_s = h[i].tolist()
+            nsq_c_next = h[i + 1][2].item() if i + 1 < n else nsq_c_final
+            costs_c.append(nll_c + self.lambda_c * math.sqrt(nsq_c) + self.lambda_s * math.sqrt(nsq_s))
+            costs_s.append(nll_s + self.lambda_c * math.sqrt(nsq_c_next) + self.lambda_s * math.sqrt(nsq_s))
+        return costs_c, costs_s
+
+
+def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, offset=None,
+          log_model=False, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2, max_iter=500,
+          betas=(0.9, 0.999), eps=1e-8, project_c=True, generator=None, Z_init=None,
+          restart=False, restart_samples=(200, 200), T_true=None, nmse_every=0,
+          use_graph=False, obs=None, tile=None, callback=None):
+    """Alternating S/C probit-MLE (qmc/qmc.ipynb :559-645).
+
+    Args mirror the notebook globals: Y (K,1,I,J) bin indices, Wx (K,1,I,J) 0/1 mask,
+    bin_boundaries / noise_std / offset of the model, lambda_c = lambda_s = 100,
+    lr_c = 5e-3, lr_s = 1e-2, max_iter = 500.  With `generator` the S-step optimises Z_init
+    through S = generator(Z) (Adam on Z, the network frozen); otherwise S is free.
+    Returns a SolveResult with S (R,1,I,J) and C (R,K) on the GPU.
+    """
+    K = Y.shape[0]
+    I, J = Y.shape[-2], Y.shape[-1]
+    if R is None:
+        R = (S_init.shape[0] if S_init is not None else
+             (C_init.shape[0] if C_init is not None else Z_init.shape[0]))
+    if obs is None:
+        obs = Observations(Y, Wx, bin_boundaries, noise_std, offset=offset or 0.0,
+                           log_model=log_model, tile=tile, R_hint=R)
+    if C_init is None:
+        C_init = torch.zeros(R, K)
+    if generator is None:
+        if S_init is None:
+            S_init = torch.zeros(R, 1, I, J)
+        sol = FreeSSolver(obs, S_init, C_init, lambda_c, lambda_s, lr_c, lr_s, betas, eps,
+                          project_c, hist_cap=max_iter)
+        nmse = []
+        done = 0
+        chunk = nmse_every if (nmse_every and T_true is not None) else max_iter
+        while done < max_iter:
+            n = min(chunk, max_iter - done)
+            sol.run(n, use_graph=use_graph)
+            done += n
+            if T_true is not None and nmse_every:
+                nmse.append(map_nmse(sol.S_pixels(), sol.C, T_true))
+            if callback is not None:
+                callback(done, sol)
+        costs_c, costs_s = sol.history()
+        return SolveResult(S=sol.S_pixels(), C=sol.C.clone(), costs_c=costs_c, costs_s=costs_s,
+                           nmse=nmse, iters=max_iter)
+    return _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c, lr_s,
+                            max_iter, betas, eps, project_c, restart, restart_samples, T_true,
+                            nmse_every, callback)
+
+
+def _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c, lr_s, max_iter,
+                     betas, eps, project_c, restart, restart_samples, T_true, nmse_every,
+                     callback, params=None, optimize_z=True):
+    """S = generator(Z) variant (qmc/qmc.ipynb :541-634).  The S-step optimises Z
+    (optimize_z) plus any extra `params` — the DIP solver passes the decoder weights."""
+    dev = obs.device
+    I, J = obs.I, obs.J
+    eng = PassEngine(obs, R, hist_cap=0)
+    C = _dev(C_init.detach().to(torch.float32)).reshape(R, obs.K).clone()
+    mC, vC = torch.zeros_like(C), torch.zeros_like(C)
+    adam_c = _lib.make_adam(lr_c, betas, eps, project_nonneg=project_c)
+    Z = Z_init.detach().to(dev, torch.float32).clone().requires_grad_(True)
+    plist = ([Z] if optimize_z else []) + list(params or [])
+    optS = torch.optim.Adam(plist, lr=lr_s, betas=betas, eps=eps)
+    with torch.no_grad():
+        S = generator(Z).reshape(R, 1, I, J)
+    S_pos = obs.to_positions(S.reshape(R, -1))
+    eng.init_state(S_pos)
+    dS_pos = torch.empty_like(S_pos)
+    costs_c, costs_s, nmse = [], [], []
+    step_c = 0
+
+    def nll_of(S_cand):
+        Sp = obs.to_positions(S_cand.reshape(R, -1))
+        eng.spass(Sp, C, 0, dS=dS_pos)
+        eng.sfinish(update_normsq=False, c_stepped=False, s_stepped=False)
+        return eng.read_state()["nll_s"]
+
+    for i in range(max_iter):
+        # ---- C-step (cost uses the S of the previous S-step, :564) ----
+        nsq_c = float((C.double() ** 2).sum())
+        eng.cpass(S_pos, C)
+        eng.cfinish(C, 1, mC=mC, vC=vC, adam=adam_c, lambda_c=lambda_c)
+        st = eng.read_state()
+        costs_c.append(st["nll_c"] + lambda_c * math.sqrt(nsq_c) + lambda_s * float(torch.norm(Z)))
+        # cfinish read step_c + 1; advance it (sfinish also reduces nothing new here)
+        eng.sfinish(update_normsq=False, c_stepped=True, s_stepped=False)
+        step_c += 1
+        # ---- one-time random restart of Z (:590-619) ----
+        if restart and i == 1:
+            best = float("inf")
+            n1, n2 = restart_samples
+            last = None
+            for _ in range(n1):
+                cand = torch.randn((R, Z.shape[1]), dtype=torch.float32)
+                with torch.no_grad():
+                    out = generator(cand.to(dev)).reshape(R, 1, I, J)
+                crit = nll_of(out) + lambda_c * float(torch.norm(C)) + lambda_s * float(torch.norm(S))
+                last = out
+                if crit < best:
+                    Z.data = cand.to(dev).clone()
+                    best = crit
+            for _ in range(n2):
+                # the reference re-evaluates the last first-round sample here (temp_out, :611)
+                cand = 0.2 * torch.randn((R, Z.shape[1]), dtype=torch.float32) + Z.detach().cpu()
+                crit = nll_of(last) + lambda_c * float(torch.norm(C)) + lambda_s * float(torch.norm(S))
+                if crit < best:
+                    Z.data = cand.to(dev).clone()
+                    best = crit
+        # ---- S-step through the generator (:622-634) ----
+        optS.zero_grad()
+        S = generator(Z).reshape(R, 1, I, J)
+        S_pos = obs.to_positions(S.detach().reshape(R, -1))
+        eng.spass(S_pos, C, 0, dS=dS_pos)
+        eng.sfinish(update_normsq=False, c_stepped=False, s_stepped=False)
+        dS = obs.to_pixels(dS_pos).reshape(R, 1, I, J)
+        reg = lambda_s * torch.norm(Z, "fro")
+        surrogate = (S * dS).sum() + reg
+        surrogate.backward()
+        optS.step()
+        st = eng.read_state()
+        costs_s.append(st["nll_s"] + lambda_c * float(torch.norm(C)) + float(reg))
+        if T_true is not None and nmse_every and (i + 1) % nmse_every == 0:
+            nmse.append(map_nmse(S.detach(), C, T_true))
+        if callback is not None:
+            callback(i + 1, dict(S=S, C=C, Z=Z))
+    return SolveResult(S=S.detach(), C=C, costs_c=costs_c, costs_s=costs_s, nmse=nmse, Z=Z.detach(),
+                       iters=max_iter)

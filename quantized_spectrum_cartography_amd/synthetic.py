@@ -1,0 +1,48 @@
+"""Synthetic one-bit / quantized radio-map problems for tests and benchmarks.
+
+`onebit_problem` follows the recipe of BASELINE.md section 3, the inputs
+the reference's CPU path is timed on: torch.manual_seed(seed) on the host CPU, then in order
+S_true = rand(R,1,I,J); C_true = rand(R,K); T_true = get_tensor(S_true, C_true);
+thr = median(T_true); sigma = (max - min)(T_true)/4; b = [0, thr, max]; Y = quantize(T_true,
+sigma, b) (linear probit, noise torch.randn on the host); Wx = bernoulli(full((K,1,I,J), f));
+S0 = 0.5*rand(R,1,I,J); C0 = 0.5*rand(R,K).  Generated on the host so that the CPU baseline
+and the GPU path see byte-identical inputs; T_true is reconstructed on the GPU when asked.
+"""
+import torch
+
+from . import _model
+
+
+def onebit_problem(I, J, K, R, f=0.1, seed=20260, device="cuda", keep_T=True):
+    g_state = torch.random.get_rng_state()
+    try:
+        torch.manual_seed(seed)
+        S_true = torch.rand(R, 1, I, J)
+        C_true = torch.rand(R, K)
+        # T_true on the GPU (bit-identical to the reference get_tensor), back to the host
+        T_true = _model.get_tensor(S_true.to(device), C_true.to(device))
+        thr = float(T_true.median())
+        tmax, tmin = float(T_true.max()), float(T_true.min())
+        sigma = (tmax - tmin) / 4
+        b = torch.tensor([0.0, thr, tmax])
+        noise = torch.randn(T_true.shape)
+        Y = _model.quantize(T_true, sigma, b, noise=noise).unsqueeze(1)
+        del noise
+        Wx = torch.bernoulli(torch.full((K, 1, I, J), f))
+        S0 = 0.5 * torch.rand(R, 1, I, J)
+        C0 = 0.5 * torch.rand(R, K)
+    finally:
+        torch.random.set_rng_state(g_state)
+    out = dict(S_true=S_true, C_true=C_true, b=b, sigma=sigma, Y=Y, Wx=Wx, S0=S0, C0=C0,
+               log_model=False, offset=0.0, thr=thr)
+    if keep_T:
+        out["T_true"] = T_true
+    return out
+
+
+CONFIGS = {
+    # name: (I, J, K, R)   BASELINE.json configs
+    "c2": (256, 256, 64, 4),
+    "c3": (512, 512, 256, 8),
+    "c4": (512, 512, 1024, 16),
+}

@@ -1,0 +1,80 @@
+"""CPU: the C-ABI library builds for gfx950, loads, and exports every symbol of include/qsc.h;
+ctypes struct layouts agree with the C compiler's.  No compute calls (no GPU here)."""
+import ctypes
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+from quantized_spectrum_cartography_amd import _build, _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def libpath():
+    return _build.build(verbose=False)
+
+
+def test_header_parses_all_entry_points():
+    h = _lib.parse_header()
+    for name in ("qsc_spass", "qsc_cpass", "qsc_cfinish", "qsc_sfinish", "qsc_quantize",
+                 "qsc_prob_probit", "qsc_reconstruct", "qsc_gram", "qsc_chol_solve",
+                 "qsc_obs_layout", "qsc_adam_step"):
+        assert name in h
+    assert len(h) >= 30
+
+
+def test_library_exports_every_declared_symbol(libpath):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", libpath]).decode()
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = sorted(set(_lib.parse_header()) - exported)
+    assert not missing, missing
+
+
+def test_library_loads_and_reports(libpath):
+    L = _lib.lib()
+    assert L.qsc_version() >= 1
+    assert L.qsc_error_string(0) == b"success"
+    assert L.qsc_error_string(_lib.QSC_EINVAL) == b"invalid argument"
+
+
+def test_code_object_targets_gfx950(libpath):
+    # the fat binary carries a gfx950 code object (bundle id amdgcn-amd-amdhsa--gfx950)
+    data = open(libpath, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_struct_layouts_match_c():
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "qsc.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(qsc_model), sizeof(qsc_adam), sizeof(qsc_obs_desc),
+         sizeof(qsc_state), offsetof(qsc_model, bounds), offsetof(qsc_obs_desc, nnz));
+  return 0;
+}
+'''
+    d = tempfile.mkdtemp()
+    c = os.path.join(d, "t.c")
+    exe = os.path.join(d, "t")
+    open(c, "w").write(src)
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+    vals = [int(x) for x in subprocess.check_output([exe]).split()]
+    assert vals[0] == ctypes.sizeof(_lib.QscModel)
+    assert vals[1] == ctypes.sizeof(_lib.QscAdam)
+    assert vals[2] == ctypes.sizeof(_lib.QscObsDesc)
+    assert vals[3] == _lib.STATE_BYTES
+    assert vals[4] == _lib.QscModel.bounds.offset
+    assert vals[5] == _lib.QscObsDesc.nnz.offset
+
+
+def test_product_fails_loudly_without_gpu():
+    import torch
+    from quantized_spectrum_cartography_amd import quantization_model as qm
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(_lib.QscError):
+        qm.get_tensor(torch.rand(2, 1, 4, 4), torch.rand(2, 3))

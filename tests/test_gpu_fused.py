@@ -1,0 +1,203 @@
+"""GPU parity of the fused passes and the alternating solver (the hot path) vs the reference
+goldens and the CPU oracle.
+
+Tolerance (north_star): recovered S, C within 1e-5 relative Frobenius of the reference CPU solver
+on identical inputs (fp32).  Single-pass NLL / gradients: 1e-5 relative."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_fro
+from oracle import explicit, reference_ops as ro, solver as osolver
+
+pytestmark = pytest.mark.gpu
+
+T = torch.from_numpy
+
+
+def _obs(Y, Wx, b, sigma, offset=0.0, log_model=False, R=4, tile=None):
+    from quantized_spectrum_cartography_amd.obs import Observations
+    return Observations(Y, Wx, b, sigma, offset=offset, log_model=log_model, R_hint=R, tile=tile)
+
+
+@pytest.mark.parametrize("name", ["pass_onebit_small", "pass_onebit_64", "pass_log_small"])
+def test_probit_nll_pass_vs_golden(golden, name):
+    from quantized_spectrum_cartography_amd import fused
+    g = golden(name)
+    R = g["S"].shape[0]
+    obs = _obs(T(g["Y"]), T(g["Wx"]), T(g["b"]), float(g["sigma"]), float(g["offset"]),
+               bool(g["log_model"]), R)
+    S = T(g["S"]).cuda().requires_grad_(True)
+    C = T(g["C"]).cuda().requires_grad_(True)
+    nll = fused.ProbitNLL.apply(S, C, obs)
+    cost = nll + float(g["lam_c"]) * torch.norm(C) + float(g["lam_s"]) * torch.norm(S)
+    cost.backward()
+    assert abs(nll.item() - float(g["nll"])) / abs(float(g["nll"])) < 1e-5
+    assert abs(cost.item() - float(g["cost"])) / abs(float(g["cost"])) < 1e-5
+    assert rel_fro(S.grad.cpu().numpy(), g["dS"]) < 1e-5
+    assert rel_fro(C.grad.cpu().numpy(), g["dC"]) < 1e-5
+
+
+def _random_case(seed, R, I, J, K, f=0.1, nbins=2, log_model=False):
+    g = torch.Generator().manual_seed(seed)
+    S = torch.rand(R, 1, I, J, generator=g)
+    C = torch.rand(R, K, generator=g)
+    Tt = ro.get_tensor(S, C)
+    if log_model:
+        b = torch.tensor([-23.025850296020508, -1.5, -0.5, 0.3, 3.0])
+        sigma = 0.7
+        off = 1e-3
+        Y = ro.quantize(Tt, sigma, b, offset=off, log_model=True,
+                        noise=torch.randn(Tt.shape, generator=g))
+    else:
+        off = 0.0
+        qs = torch.quantile(Tt.reshape(-1)[:100000], torch.linspace(0, 1, nbins + 1))
+        b = qs.clone()
+        sigma = (float(Tt.max()) - float(Tt.min())) / 4
+        Y = ro.quantize(Tt, sigma, b, noise=torch.randn(Tt.shape, generator=g))
+    Wx = torch.bernoulli(torch.full((K, 1, I, J), f), generator=g)
+    S0 = 0.5 * torch.rand(R, 1, I, J, generator=g) + (0.25 if log_model else 0.0)
+    C0 = 0.5 * torch.rand(R, K, generator=g)
+    return dict(Y=Y.unsqueeze(1), Wx=Wx, b=b, sigma=sigma, offset=off, S0=S0, C0=C0, T=Tt,
+                log_model=log_model)
+
+
+@pytest.mark.parametrize("seed,R,I,J,K,f,nbins,log_model,tile", [
+    (1, 1, 13, 11, 3, 0.5, 2, False, None),       # tiny, ragged (P not a multiple of 64)
+    (2, 3, 40, 40, 70, 0.1, 2, False, None),      # K > 64: two k-slices, ragged k
+    (3, 8, 64, 64, 256, 0.1, 2, False, 512),      # C3 shape class
+    (4, 16, 48, 50, 33, 0.2, 2, False, 192),      # R = 16 (max), wide tiles
+    (5, 4, 32, 32, 16, 0.3, 5, False, None),      # multi-bin linear
+    (6, 4, 32, 32, 16, 0.3, 4, True, None),       # log model
+    (7, 2, 51, 51, 64, 1.0, 2, False, None),      # f = 1 (config-1 mask), all observed
+])
+def test_fused_pass_vs_explicit(seed, R, I, J, K, f, nbins, log_model, tile):
+    from quantized_spectrum_cartography_amd import fused
+    d = _random_case(seed, R, I, J, K, f, nbins, log_model)
+    obs = _obs(d["Y"], d["Wx"], d["b"], d["sigma"], d["offset"], log_model, R, tile)
+    st = obs.stats()
+    assert st["nnz"] == int(d["Wx"].sum())
+    S = d["S0"].cuda().requires_grad_(True)
+    C = d["C0"].cuda().requires_grad_(True)
+    nll = fused.ProbitNLL.apply(S, C, obs)
+    nll.backward()
+    P = I * J
+    rn, rdS, rdC = explicit.nll_grad(d["S0"].reshape(R, P).numpy(), d["C0"].numpy(),
+                                     d["Y"].reshape(K, P).numpy(), d["Wx"].reshape(K, P).numpy(),
+                                     d["b"].numpy(), d["sigma"], d["offset"], log_model)
+    assert abs(nll.item() - rn) / abs(rn) < 1e-5
+    assert rel_fro(S.grad.cpu().reshape(R, P).numpy(), rdS) < 1e-5
+    assert rel_fro(C.grad.cpu().numpy(), rdC) < 1e-5
+
+
+def test_fused_pass_deterministic():
+    from quantized_spectrum_cartography_amd import fused
+    d = _random_case(11, 8, 64, 64, 128)
+    obs = _obs(d["Y"], d["Wx"], d["b"], d["sigma"], R=8)
+    outs = []
+    for _ in range(3):
+        S = d["S0"].cuda().requires_grad_(True)
+        C = d["C0"].cuda().requires_grad_(True)
+        nll = fused.ProbitNLL.apply(S, C, obs)
+        nll.backward()
+        outs.append((nll.item(), S.grad.cpu().numpy(), C.grad.cpu().numpy()))
+    for o in outs[1:]:
+        assert o[0] == outs[0][0]
+        assert np.array_equal(o[1], outs[0][1]) and np.array_equal(o[2], outs[0][2])
+
+
+@pytest.mark.parametrize("name", ["solve_onebit_64", "solve_log_32"])
+def test_solver_vs_reference_golden(golden, name):
+    """Free-S alternating solver (qmc/qmc.ipynb :559-634) after 1 and 10 outer iterations."""
+    from quantized_spectrum_cartography_amd import qmc
+    g = golden(name)
+    n = int(g["n_iter"])
+    Y = T(g["Y"].astype(np.int64))
+    Wx = T(g["Wx"].astype(np.float32))
+    kw = dict(offset=float(g["offset"]), log_model=bool(g["log_model"]),
+              lambda_c=float(g["lam_c"]), lambda_s=float(g["lam_s"]), lr_c=float(g["lr_c"]),
+              lr_s=float(g["lr_s"]))
+    r1 = qmc.solve(Y, Wx, T(g["b"]), float(g["sigma"]), S_init=T(g["S0"]), C_init=T(g["C0"]),
+                   max_iter=1, **kw)
+    assert rel_fro(r1.S.cpu().numpy(), g["S_it1"]) < 1e-5
+    assert rel_fro(r1.C.cpu().numpy(), g["C_it1"]) < 1e-5
+    rn = qmc.solve(Y, Wx, T(g["b"]), float(g["sigma"]), S_init=T(g["S0"]), C_init=T(g["C0"]),
+                   max_iter=n, **kw)
+    assert rel_fro(rn.S.cpu().numpy(), g["S_it%d" % n]) < 1e-5
+    assert rel_fro(rn.C.cpu().numpy(), g["C_it%d" % n]) < 1e-5
+    assert np.allclose(rn.costs_c, g["costs_c"], rtol=1e-5)
+    assert np.allclose(rn.costs_s, g["costs_s"], rtol=1e-5)
+
+
+def test_solver_graph_replay_matches_eager():
+    from quantized_spectrum_cartography_amd import qmc
+    d = _random_case(21, 4, 64, 64, 64)
+    a = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], S_init=d["S0"], C_init=d["C0"], max_iter=20)
+    b = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], S_init=d["S0"], C_init=d["C0"], max_iter=20,
+                  use_graph=True)
+    assert np.array_equal(a.S.cpu().numpy(), b.S.cpu().numpy())
+    assert np.array_equal(a.C.cpu().numpy(), b.C.cpu().numpy())
+
+
+def test_solver_vs_oracle_random_sizes():
+    from quantized_spectrum_cartography_amd import qmc
+    for seed, R, I, J, K in [(31, 3, 37, 29, 90), (32, 8, 64, 64, 256)]:
+        d = _random_case(seed, R, I, J, K)
+        res = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], S_init=d["S0"], C_init=d["C0"],
+                        max_iter=5)
+        ref = osolver.free_s_solve(d["S0"], d["C0"], d["Y"], d["Wx"], d["b"], d["sigma"], n_iter=5)
+        assert rel_fro(res.S.cpu().numpy(), ref["S"].numpy()) < 1e-5
+        assert rel_fro(res.C.cpu().numpy(), ref["C"].numpy()) < 1e-5
+
+
+def test_mat_fixture_onebit_solve(golden):
+    """Config 1 (qmc/onebitdata1.mat, R = 2, f = 1 via Om): one-bit variant, GPU vs oracle."""
+    from quantized_spectrum_cartography_amd import qmc
+    g = golden("mat_c1")
+    K = g["T"].shape[0]
+    Y = T(((g["T"].astype(np.int64) + 1) // 2)).unsqueeze(1)
+    Wx = torch.ones(K, 1, 51, 51)
+    b = torch.tensor([0.0, 0.0045, float(g["T_true"].max())])
+    sigma = 0.02
+    gen = torch.Generator().manual_seed(5)
+    S0 = 0.5 * torch.rand(2, 1, 51, 51, generator=gen)
+    C0 = 0.5 * torch.rand(2, K, generator=gen)
+    res = qmc.solve(Y, Wx, b, sigma, S_init=S0, C_init=C0, max_iter=5)
+    ref = osolver.free_s_solve(S0, C0, Y, Wx, b, sigma, n_iter=5)
+    assert rel_fro(res.S.cpu().numpy(), ref["S"].numpy()) < 1e-5
+    assert rel_fro(res.C.cpu().numpy(), ref["C"].numpy()) < 1e-5
+
+
+def test_generator_solver_runs_and_decreases_cost():
+    from quantized_spectrum_cartography_amd import nets, qmc
+    from quantized_spectrum_cartography_amd.utils import LOG_OFFSET_4, QUANTIZATION_BOUNDARIES_4_BINS_LOG
+    torch.manual_seed(0)
+    R, K = 2, 64
+    gen = nets.Generator256().cuda().eval()
+    S_true = torch.rand(R, 1, 51, 51) ** 4 * 0.2
+    C_true = torch.rand(R, K)
+    Tt = ro.get_tensor(S_true, C_true)
+    Y = ro.quantize(Tt, 5.0, torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG), offset=LOG_OFFSET_4,
+                    log_model=True).unsqueeze(1)
+    Wx = torch.bernoulli(torch.full((K, 1, 51, 51), 0.1))
+    res = qmc.solve(Y, Wx, torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG), 5.0, R=R,
+                    offset=LOG_OFFSET_4, log_model=True, generator=gen, Z_init=torch.randn(R, 256),
+                    C_init=torch.zeros(R, K), max_iter=6, restart=True, restart_samples=(5, 5))
+    assert res.S.shape == (R, 1, 51, 51)
+    assert np.all(np.isfinite(res.costs_s)) and res.costs_s[-1] < res.costs_s[0]
+
+
+def test_dip_solver_256():
+    from quantized_spectrum_cartography_amd import dip
+    from quantized_spectrum_cartography_amd.utils import QUANTIZATION_BOUNDARIES_4_BINS_LOG
+    torch.manual_seed(1)
+    R, K, N = 2, 8, 64
+    S_true = torch.rand(R, 1, N, N) * 0.2
+    C_true = torch.rand(R, K)
+    Tt = ro.get_tensor(S_true, C_true)
+    b = torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG)
+    Y = ro.quantize(Tt, 5.0, b, offset=1e-10, log_model=True).unsqueeze(1)
+    Wx = torch.bernoulli(torch.full((K, 1, N, N), 0.1))
+    res = dip.solve(Y, Wx, b, 5.0, R, offset=1e-10, max_iter=4)
+    assert res.S.shape == (R, 1, N, N)
+    assert np.all(np.isfinite(res.costs_c))
