@@ -70,24 +70,38 @@ typedef struct qsc_adam {
 } qsc_adam;
 
 /* Device-resident solver scalars (one struct per solve, caller-allocated device memory,
- * zero-initialised by qsc_state_init). Kernels read and write it; host reads it back only
- * when it wants the cost history. */
+ * initialised by qsc_state_init).  Kernels read and write it; the host reads it back only
+ * when it wants the cost history.  Book-keeping protocol (no extra launches per iteration):
+ * every block of a kernel reads the counters it needs at its start; the one-thread updates
+ * are deferred to the NEXT kernel of the other block type through `pending`:
+ *   cfinish (mode 1) sets QSC_PEND_C; the next qsc_spass applies step_c += 1;
+ *   qsc_spass sets QSC_PEND_SNLL (and qsc_spass mode 1 / qsc_supdate set QSC_PEND_SUPD);
+ *   the next qsc_cfinish (or qsc_state_flush) reduces the S-side partials into nll_s /
+ *   normsq_s, applies step_s += 1 and appends the history row of that iteration. */
+#define QSC_PEND_C 1
+#define QSC_PEND_SNLL 2
+#define QSC_PEND_SUPD 4
 typedef struct qsc_state {
   int32_t step_c;   /* Adam steps taken on C */
   int32_t step_s;   /* Adam steps taken on S */
-  int32_t iter;     /* completed outer iterations */
-  int32_t pad_;
+  int32_t iter;     /* S-passes issued (outer iterations) */
+  int32_t pending;  /* QSC_PEND_* flags, see above */
   float normsq_s;   /* ||S||_F^2 of the current S */
-  float normsq_c;   /* ||C||_F^2 of the current C (before the last C update) */
+  float normsq_c;   /* ||C||_F^2 of C before the last C update */
   float nll_c;      /* NLL of the last C-pass   (-sum Wx log P, qmc/qmc.ipynb :572) */
   float nll_s;      /* NLL of the last S-pass */
-  float reserved[8];
+  float normsq_s_prev; /* ||S||^2 the last S-pass was evaluated with */
+  float reserved[7];
 } qsc_state;
 
 /* Packed observation layout, produced by qsc_obs_layout (host struct).
  * Positions q in 0..Pp-1 are pixels re-ordered by observation count (perm[q] = pixel).
- *  S-format ("pixel slices"): for slice s (64 positions), lane l, entry j < s_width[s]:
- *     idx = s_off[s] + (j/4)*256 + l*4 + (j%4);  value = k | code << KBITS  (code PAD = pad)
+ *  S-format ("pixel slices"): for slice s (QSC_SLICE = 32 positions), position l in the slice,
+ *     entry j < s_width[s]:
+ *     idx = s_off[s] + (j/4)*128 + l*4 + (j%4);  value = k | code << KBITS  (code PAD = pad)
+ *     (the S-pass gives each pixel two lanes, which take alternate 4-entry chunks) */
+#define QSC_SLICE 32
+/*
  *  C-format ("frequency slices" per pixel tile): tile t (PT positions), k-slice ks (64 k's),
  *     lane l (k = 64*ks + l), entry j < c_width[t*nks+ks]:
  *     idx = c_off[t*nks+ks] + (j/4)*256 + l*4 + (j%4);  value = qlocal | code << QBITS
@@ -96,7 +110,7 @@ typedef struct qsc_state {
 typedef struct qsc_obs_desc {
   int32_t K;      /* frequency bins in this (local) slab */
   int32_t P;      /* pixels I*J */
-  int32_t Pp;     /* P rounded up to 64 */
+  int32_t Pp;     /* P rounded up to PT */
   int32_t PT;     /* C-pass pixel tile (positions), multiple of 64, <= 4096 when narrow */
   int32_t ntiles; /* Pp / PT */
   int32_t nks;    /* ceil(K / 64) */
@@ -180,12 +194,13 @@ QSC_API int qsc_sumsq(const float* x, int64_t n, float* out, void* ws, size_t ws
  * ------------------------------------------------------------------------------------- */
 /* cnt[p] = number of observed k for pixel p (async) */
 QSC_API int qsc_obs_count(const uint8_t* codes, int32_t K, int32_t P, int32_t* cnt, void* stream);
-/* perm[q] = pixels sorted by cnt descending, stable; positions q >= P are padding (-1). */
+/* perm[q] = pixels sorted by cnt descending, stable; positions P <= q < Pp are padding (-1).
+ * Pp = P rounded up to the C-pass tile PT (a multiple of 64). */
 QSC_API size_t qsc_obs_order_workspace_bytes(int32_t P);
-QSC_API int qsc_obs_order(const int32_t* cnt, int32_t P, int32_t* perm, void* ws,
+QSC_API int qsc_obs_order(const int32_t* cnt, int32_t P, int32_t Pp, int32_t* perm, void* ws,
                           size_t ws_bytes, void* stream);
 /* SYNCHRONOUS: computes slice widths/offsets of both formats and fills *desc.
- * s_width[Pp/64], s_off[Pp/64 + 1], c_width[ntiles*nks], c_off[ntiles*nks + 1]. */
+ * s_width[Pp/QSC_SLICE], s_off[Pp/QSC_SLICE + 1], c_width[ntiles*nks], c_off[ntiles*nks + 1]. */
 QSC_API size_t qsc_obs_layout_workspace_bytes(int32_t K, int32_t P, int32_t PT);
 QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t PT, int32_t nbins,
                            const int32_t* perm, const int32_t* cnt, int32_t* s_width,
@@ -211,11 +226,12 @@ QSC_API int qsc_perm_scatter(const float* pos, const int32_t* perm, int32_t R, i
  * S, mS, vS, dS are in position order [R][Pp]; C, mC, vC in [R][K].
  * ------------------------------------------------------------------------------------- */
 QSC_API size_t qsc_pass_workspace_bytes(const qsc_obs_desc* d, int32_t R);
+/* zero the state; normsq_s = ||S||^2 of the initial S (S nullable: 0) */
 QSC_API int qsc_state_init(qsc_state* st, const float* S, int32_t R, int32_t Pp, void* ws,
                            size_t ws_bytes, void* stream);
 /* S-pass.  mode 0: write dS (NLL gradient only, no regulariser) — used by the generator/DIP
  * solvers and K-slab sharding; mode 1: fused S-step — dS + lambda_s*S/||S|| then Adam on S
- * (S, mS, vS updated in place).  Writes per-block partials into ws. */
+ * (S, mS, vS updated in place).  Writes per-slice partials into ws (see qsc_state). */
 QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
                       const int64_t* s_off, const qsc_model* m, int32_t R, float* S,
                       const float* C, int32_t mode, float* dS, float* mS, float* vS,
@@ -225,28 +241,29 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
 QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_t* c_width,
                       const int64_t* c_off, const qsc_model* m, int32_t R, const float* S,
                       const float* C, void* ws, size_t ws_bytes, void* stream);
-/* reduce the C-pass slab.  mode 0: write dC (NLL gradient only); mode 1: fused C-step:
- * dC + lambda_c*C/||C||, Adam on C, projection; also records st->nll_c, st->normsq_c.
+/* reduce the C-pass slab (fixed order).  mode 0: write dC (NLL gradient only); mode 1: fused
+ * C-step: dC + lambda_c*C/||C||, Adam on C, projection.  Block 0 also records nll_c /
+ * normsq_c and settles a pending S-pass (see qsc_state), appending history row
+ * [nll_c, nll_s, normsq_c, normsq_s] of each completed iteration to hist (nullable).
  * normsq_c_ext (device, nullable): global ||C||^2 supplied by the caller (K-slab sharding). */
 QSC_API int qsc_cfinish(const qsc_obs_desc* d, int32_t R, float* C, int32_t mode, float* dC,
                         float* mC, float* vC, const qsc_adam* adam, float lambda_c,
-                        const float* normsq_c_ext, qsc_state* st, void* ws, size_t ws_bytes,
-                        void* stream);
-/* reduce the S-pass partials into st (nll_s, normsq_s of the updated S), advance counters,
- * append [nll_c, nll_s, normsq_c, normsq_s] to hist[4*iter] (hist nullable). */
-QSC_API int qsc_sfinish(const qsc_obs_desc* d, int32_t R, qsc_state* st, float* hist,
+                        const float* normsq_c_ext, qsc_state* st, float* hist,
                         int32_t hist_cap, void* ws, size_t ws_bytes, void* stream);
-/* as qsc_sfinish with explicit flags: update_normsq (S was updated by the fused S-step),
- * c_stepped / s_stepped (advance the Adam step counters of C / S). */
-QSC_API int qsc_sfinish_ex(const qsc_obs_desc* d, int32_t R, qsc_state* st, float* hist,
-                           int32_t hist_cap, int32_t update_normsq, int32_t c_stepped,
-                           int32_t s_stepped, void* ws, size_t ws_bytes, void* stream);
-/* plain Adam (torch.optim.Adam single-tensor semantics) with optional regulariser
- * g += lambda * x / sqrt(*normsq) and projection; step counter taken from *step (+1, read
- * only).  Used after an all-reduce of dS (K-slab sharding). */
-QSC_API int qsc_adam_step(float* x, float* mx, float* vx, const float* g, int64_t n,
-                          const qsc_adam* adam, const int32_t* step, float lambda,
-                          const float* normsq, void* stream);
+/* settle everything pending in st (S-pass partials, counters, history) — one block; used at
+ * the end of a solve and between passes that are not followed by a qsc_cfinish. */
+QSC_API int qsc_state_flush(const qsc_obs_desc* d, int32_t R, qsc_state* st, float* hist,
+                            int32_t hist_cap, void* ws, size_t ws_bytes, void* stream);
+/* S update from an externally reduced gradient g [R][Pp] (K-slab sharding, after the RCCL
+ * all-reduce of the partial dS): g + lambda_s*S/||S||, Adam on S, ||S_new||^2 partials, with
+ * the same state protocol as the fused qsc_spass mode 1. */
+QSC_API int qsc_supdate(const qsc_obs_desc* d, int32_t R, float* S, float* mS, float* vS,
+                        const float* g, const qsc_adam* adam, float lambda_s, qsc_state* st,
+                        void* ws, size_t ws_bytes, void* stream);
+/* ||x||^2 into *out (fp32, fixed order), e.g. the local ||C_slab||^2 before an all-reduce */
+QSC_API int qsc_sumsq_small(const float* x, int32_t n, float* out, void* stream);
+/* diagnostics: out[0..n) = ocml erff(x), out[n..2n) = the branch-free erf of the passes */
+QSC_API int qsc_selftest_erf(const float* x, int32_t n, float* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * R x R normal equations (MFMA): backup/algorithms/NMF_SPA.m:18-19 pseudo-inverse and

@@ -47,3 +47,57 @@ def free_s_solve(S0, C0, Y, Wx, b, sigma, offset=0.0, log_model=False, n_iter=10
             break
     return dict(S=S.detach(), C=C.detach(), costs_c=costs_c, costs_s=costs_s, snaps=snaps,
                 step_times=step_times)
+
+
+def generator_solve(generator, Z0, C0, Y, Wx, b, sigma, offset=0.0, log_model=False, n_iter=5,
+                    lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2, restart=False,
+                    restart_samples=(200, 200)):
+    """qmc/qmc.ipynb :541-634 verbatim in structure: S = generator(Z) (network frozen, Adam on Z),
+    the C-step uses the S of the previous S-step, one random restart of Z at i == 1 whose
+    second round re-evaluates the last first-round sample (temp_out, :611)."""
+    R = Z0.shape[0]
+    I, J = Y.shape[-2], Y.shape[-1]
+    C = C0.clone().requires_grad_(True)
+    Z = Z0.clone().requires_grad_(True)
+    optC = torch.optim.Adam([C], lr=lr_c)
+    optZ = torch.optim.Adam([Z], lr=lr_s)
+    with torch.no_grad():
+        S = generator(Z).reshape(R, 1, I, J)
+    costs_c, costs_s = [], []
+    for i in range(n_iter):
+        Sc = S.detach().clone()
+        optC.zero_grad()
+        nll = ro.masked_nll(Sc, C, Y, Wx, b, sigma, offset, log_model)
+        cost = nll + lambda_c * torch.norm(C, "fro") + lambda_s * torch.norm(Z, "fro")
+        cost.backward()
+        optC.step()
+        with torch.no_grad():
+            C[C < 0] = 0
+        costs_c.append(cost.item())
+        if restart and i == 1:
+            best = 9999999
+            n1, n2 = restart_samples
+            with torch.no_grad():
+                for _ in range(n1):
+                    temp = torch.randn((R, Z.shape[1]), dtype=torch.float32)
+                    temp_out = generator(temp).reshape(R, 1, I, J)
+                    crit = (ro.masked_nll(temp_out, C, Y, Wx, b, sigma, offset, log_model)
+                            + lambda_c * torch.norm(C, "fro") + lambda_s * torch.norm(S, "fro"))
+                    if crit < best:
+                        Z.data = temp.clone()
+                        best = crit
+                for _ in range(n2):
+                    temp = 0.2 * torch.randn((R, Z.shape[1]), dtype=torch.float32) + Z
+                    crit = (ro.masked_nll(temp_out, C, Y, Wx, b, sigma, offset, log_model)
+                            + lambda_c * torch.norm(C, "fro") + lambda_s * torch.norm(S, "fro"))
+                    if crit < best:
+                        Z.data = temp.clone()
+                        best = crit
+        optZ.zero_grad()
+        S = generator(Z).reshape(R, 1, I, J)
+        nll = ro.masked_nll(S, C, Y, Wx, b, sigma, offset, log_model)
+        cost = nll + lambda_c * torch.norm(C, "fro") + lambda_s * torch.norm(Z, "fro")
+        cost.backward()
+        optZ.step()
+        costs_s.append(cost.item())
+    return dict(S=S.detach(), C=C.detach(), Z=Z.detach(), costs_c=costs_c, costs_s=costs_s)

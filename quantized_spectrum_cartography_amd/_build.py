@@ -15,8 +15,11 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libqsc_hip.so")
 SOURCES = ["qsc_ops.hip", "qsc_obs.hip", "qsc_pass.hip", "qsc_gram.hip"]
 ARCH = os.environ.get("QSC_OFFLOAD_ARCH", "gfx950")
+# -ffp-contract=off: hipcc contracts a*b+c into FMA by default, which would change the
+# reference's separately rounded products and sums (get_tensor, quantize); FMAs that are
+# wanted are written explicitly with __builtin_fmaf.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall",
-          "-Wno-unused-function"]
+          "-Wno-unused-function", "-ffp-contract=off"]
 
 
 def _hipcc():

@@ -17,6 +17,7 @@ HEADER = os.path.join(os.path.dirname(_build.PKG_DIR), "include", "qsc.h")
 
 QSC_MAX_BOUNDS = 256
 QSC_MAX_R = 16
+QSC_SLICE = 32  # S-format slice (pixel positions per list group), include/qsc.h
 QSC_EINVAL = 100000
 UNOBSERVED = 0xFF
 
@@ -40,9 +41,11 @@ class QscObsDesc(ctypes.Structure):
                 ("s_entries", ctypes.c_int64), ("c_entries", ctypes.c_int64)]
 
 
-# device-resident qsc_state: 4 int32 + 4 float + 8 float
+# device-resident qsc_state: 4 int32 + 5 float + 7 reserved float
 STATE_BYTES = 64
-STATE_FIELDS = ("step_c", "step_s", "iter", "pad_", "normsq_s", "normsq_c", "nll_c", "nll_s")
+STATE_FIELDS = ("step_c", "step_s", "iter", "pending", "normsq_s", "normsq_c", "nll_c", "nll_s",
+                "normsq_s_prev")
+STATE_OFFSETS = {name: 4 * i for i, name in enumerate(STATE_FIELDS)}
 
 _HOST_STRUCTS = {"qsc_model": QscModel, "qsc_adam": QscAdam, "qsc_obs_desc": QscObsDesc}
 _SCALARS = {"int": ctypes.c_int, "int32_t": ctypes.c_int32, "int64_t": ctypes.c_int64,
@@ -95,12 +98,13 @@ def lib():
     with _lock:
         if _lib is not None:
             return _lib
-        if not os.path.exists(_build.LIB_PATH):
+        path = os.environ.get("QSC_LIB_PATH", _build.LIB_PATH)  # variant builds (tuning)
+        if not os.path.exists(path):
             try:
                 _build.build(verbose=False)
             except Exception as e:  # pragma: no cover - depends on toolchain
                 raise QscError("libqsc_hip.so is missing and could not be built: %s" % e)
-        L = ctypes.CDLL(_build.LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         for name, (res, args) in parse_header().items():
             fn = getattr(L, name)
             fn.restype = res
@@ -172,5 +176,11 @@ def read_state(st):
     """Decode a device qsc_state tensor (uint8[64]) into a dict (synchronises)."""
     raw = st.detach().cpu()
     ints = raw[:16].view(torch.int32).tolist()
-    flts = raw[16:32].view(torch.float32).tolist()
+    flts = raw[16:36].view(torch.float32).tolist()
     return dict(zip(STATE_FIELDS, ints + flts))
+
+
+def state_field(st, name):
+    """A 1-element device view of one float field of a qsc_state tensor."""
+    o = STATE_OFFSETS[name]
+    return st[o:o + 4].view(torch.float32)

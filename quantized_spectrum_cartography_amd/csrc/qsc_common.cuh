@@ -108,6 +108,112 @@ __device__ __forceinline__ void probit_lik(float x, float lo, float hi, bool lo_
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Branch-free erf with the exact operation sequence of ROCm's ocml erff (ROCm 7.2,
+// read back from its gfx950 ISA): |x| < 1 -> x + x*poly(x^2); |x| >= 1 -> 1 - exp(-p(|x|))
+// with ocml's two-part exp; sign copied from x.  Bitwise identical to erff, but both halves
+// are evaluated and selected so that a wavefront never diverges on |x| and the compiler can
+// interleave independent entries.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ float bits(uint32_t u) { return __uint_as_float(u); }
+
+__device__ __forceinline__ float erf_bf(float x) {
+  const float ax = fabsf(x);
+  // |x| >= 1 branch
+  float p = __builtin_fmaf(ax, bits(0x378e98abu), bits(0xb9c68948u));
+  p = __builtin_fmaf(ax, p, bits(0x3b7cd369u));
+  p = __builtin_fmaf(ax, p, bits(0xbcc618b2u));
+  p = __builtin_fmaf(ax, p, bits(0x3dda74e4u));
+  p = __builtin_fmaf(ax, p, bits(0x3f228afdu));
+  p = __builtin_fmaf(ax, p, bits(0x3e03c728u));
+  p = __builtin_fmaf(ax, p, ax);
+  // exp(-p), ocml expf: hi/lo split of -log2(e), round, exp2, ldexp, range selects
+  const float nl2e = bits(0xbfb8aa3bu);
+  const float h = p * nl2e;
+  float l = __builtin_fmaf(p, nl2e, -h);
+  const float n = __builtin_rintf(h);
+  l = __builtin_fmaf(p, bits(0xb2a5705fu), l);
+  float r = __builtin_amdgcn_exp2f((h - n) + l);
+  r = __builtin_amdgcn_ldexpf(r, (int)n);
+  r = !(p > bits(0x42ce8ed0u)) ? r : 0.0f;             // NaN keeps r (v_cmp_nlt)
+  r = !(p < bits(0xc2b17218u)) ? r : __builtin_inff();  // (v_cmp_ngt)
+  const float big = 1.0f - r;
+  // |x| < 1 branch
+  const float t = x * x;
+  float q = __builtin_fmaf(bits(0xba1345e1u), t, bits(0x3ba10414u));
+  q = __builtin_fmaf(t, q, bits(0xbcdac9b8u));
+  q = __builtin_fmaf(t, q, bits(0x3de703beu));
+  q = __builtin_fmaf(t, q, bits(0xbec09330u));
+  q = __builtin_fmaf(t, q, bits(0x3e0375d0u));
+  const float small = __builtin_fmaf(ax, q, ax);
+  const float m = (ax < 1.0f) ? small : big;  // NaN takes the |x| >= 1 path, as in ocml
+  return __builtin_copysignf(m, x);
+}
+
+// Per-call constants of the fused passes.
+struct Lik {
+  float a, inv_a, kgrad, offset;
+  float thr;      // b[1]: the single active edge of the saturated one-bit model
+};
+
+inline Lik make_lik(const qsc_model* m) {
+  const Probit p = make_probit(m);
+  Lik l;
+  l.a = p.a;
+  l.inv_a = p.inv_a;
+  l.kgrad = p.kgrad;
+  l.offset = p.offset;
+  l.thr = m->nbounds >= 2 ? m->bounds[1] : 0.0f;
+  return l;
+}
+
+// Fused-pass likelihood kinds: one active edge (linear one-bit with saturated +-1e5 outer
+// edges: P = F(thr - x) for code 0, 1 - F(thr - x) for code 1, exactly the reference's values),
+// or the general two-edge form (multi-bin and/or log model).
+enum { LIK_ONEBIT = 0, LIK_GENERAL = 1 };
+
+inline int lik_kind(const qsc_model* m) {
+  const Probit p = make_probit(m);
+  return (m->log_model == 0 && m->nbounds == 3 && p.lo_sat && p.hi_sat) ? LIK_ONEBIT : LIK_GENERAL;
+}
+
+__device__ __forceinline__ float div_lik(float x, const Lik& c) {
+  const float q = x * c.inv_a;
+  const float r = __builtin_fmaf(-q, c.a, x);
+  return __builtin_fmaf(r, c.inv_a, q);
+}
+
+// One observed entry: t = reconstruction value; returns log P and g = d(-log P)/dt.
+// Branch-free; `edges` is only read by the general kind.
+template <int KIND, bool LOG>
+__device__ __forceinline__ void lik_grad(float t, int code, const float2* __restrict__ edges,
+                                         const Lik& c, float& logP, float& g) {
+  if (KIND == LIK_ONEBIT) {
+    const float z = div_lik(c.thr - t, c);
+    const float F = 0.5f * (1.0f + erf_bf(z));
+    const bool c0 = (code == 0);
+    const float P = c0 ? F : 1.0f - F;
+    const float e = __expf(-z * z) * c.kgrad;
+    const float rp = __builtin_amdgcn_rcpf(P);
+    g = (c0 ? e : -e) * rp;
+    logP = __logf(P);
+  } else {
+    float x = t, tinv = 1.0f;
+    if (LOG) {
+      const float tp = t + c.offset;
+      x = logf(tp);
+      tinv = __builtin_amdgcn_rcpf(tp);
+    }
+    const float2 e2 = edges[code];
+    const float u = div_lik(e2.y - x, c);
+    const float w = div_lik(e2.x - x, c);
+    const float P = 0.5f * (1.0f + erf_bf(u)) - 0.5f * (1.0f + erf_bf(w));
+    const float d = (__expf(-u * u) - __expf(-w * w)) * c.kgrad;
+    g = d * __builtin_amdgcn_rcpf(P) * tinv;
+    logP = __logf(P);
+  }
+}
+
 // One observed entry end to end: t is the linear reconstruction value; returns P and the
 // gradient of -log P w.r.t. t (chain rule through log(t + offset) in the log model).
 __device__ __forceinline__ void entry_grad(float t, int code, const float2* edges,
@@ -166,11 +272,23 @@ struct AdamScalars {
   float eps;        // fp32(eps)        (add_ scalar)
 };
 
+// beta^step for an integer step by binary powering in double (within an ulp of libm pow; the
+// fp32 values derived from it match torch's).  Small register footprint, unlike ocml pow().
+__device__ __noinline__ double ipow(double b, int n) {
+  double r = 1.0;
+  while (n > 0) {
+    if (n & 1) r *= b;
+    b *= b;
+    n >>= 1;
+  }
+  return r;
+}
+
 __device__ __forceinline__ AdamScalars adam_scalars(const qsc_adam& ad, int step) {
   AdamScalars s;
   const double b1 = ad.beta1, b2 = ad.beta2;
-  const double bc1 = 1.0 - pow(b1, (double)step);
-  const double bc2 = 1.0 - pow(b2, (double)step);
+  const double bc1 = 1.0 - ipow(b1, step);
+  const double bc2 = 1.0 - ipow(b2, step);
   s.step_size = (float)(ad.lr / bc1);
   s.beta2 = (float)b2;
   s.eps = (float)ad.eps;

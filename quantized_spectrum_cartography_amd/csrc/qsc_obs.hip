@@ -36,7 +36,7 @@ __global__ void fill_int_kernel(int* __restrict__ v, int n, int val) {
   if (i < n) v[i] = val;
 }
 
-// S-format slice widths: 64 * round4(max count in the slice)
+// S-format slice widths: QSC_SLICE * round4(max count in the slice)
 __global__ void __launch_bounds__(kBlock) s_width_kernel(const int* __restrict__ perm,
                                                          const int* __restrict__ cnt, int P,
                                                          int nslices, int* __restrict__ width,
@@ -44,13 +44,13 @@ __global__ void __launch_bounds__(kBlock) s_width_kernel(const int* __restrict__
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nslices) return;
   int m = 0;
-  for (int l = 0; l < 64; ++l) {
-    const int p = perm[s * 64 + l];
+  for (int l = 0; l < QSC_SLICE; ++l) {
+    const int p = perm[s * QSC_SLICE + l];
     if (p >= 0 && p < P) m = max(m, cnt[p]);
   }
   m = (m + 3) & ~3;
   width[s] = m;
-  sizes[s] = (int64_t)m * 64;
+  sizes[s] = (int64_t)m * QSC_SLICE;
 }
 
 // C-format per (tile, k) counts via LDS integer atomics (order-independent), then widths.
@@ -92,8 +92,9 @@ struct EntryTraits<uint32_t> {
   static constexpr uint32_t kPad = 255;
 };
 
-__device__ __forceinline__ int64_t slot(int64_t base, int lane, int j) {
-  return base + (int64_t)(j >> 2) * 256 + lane * 4 + (j & 3);
+// chunked column-major slot of entry j of lane `lane` in a list group of `lanes` lanes
+__device__ __forceinline__ int64_t slot(int64_t base, int lanes, int lane, int j) {
+  return base + (int64_t)(j >> 2) * (lanes * 4) + lane * 4 + (j & 3);
 }
 
 template <typename E>
@@ -106,7 +107,7 @@ __global__ void __launch_bounds__(kBlock) s_fill_kernel(const uint8_t* __restric
   using Tr = EntryTraits<E>;
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= Pp) return;
-  const int s = q >> 6, lane = q & 63;
+  const int s = q / QSC_SLICE, lane = q % QSC_SLICE;
   const int W = width[s];
   const int64_t base = off[s];
   const int p = perm[q];
@@ -114,10 +115,11 @@ __global__ void __launch_bounds__(kBlock) s_fill_kernel(const uint8_t* __restric
   if (p >= 0 && p < P) {
     for (int k = 0; k < K; ++k) {
       const uint8_t c = codes[(int64_t)k * P + p];
-      if (c != QSC_UNOBSERVED) ent[slot(base, lane, j++)] = (E)((uint32_t)k | ((uint32_t)c << Tr::kBits));
+      if (c != QSC_UNOBSERVED)
+        ent[slot(base, QSC_SLICE, lane, j++)] = (E)((uint32_t)k | ((uint32_t)c << Tr::kBits));
     }
   }
-  for (; j < W; ++j) ent[slot(base, lane, j)] = (E)(Tr::kPad << Tr::kBits);
+  for (; j < W; ++j) ent[slot(base, QSC_SLICE, lane, j)] = (E)(Tr::kPad << Tr::kBits);
 }
 
 template <typename E>
@@ -140,10 +142,11 @@ __global__ void __launch_bounds__(kBlock) c_fill_kernel(const uint8_t* __restric
         const int p = perm[(int64_t)t * PT + ql];
         if (p < 0 || p >= P) continue;
         const uint8_t c = codes[(int64_t)kk * P + p];
-        if (c != QSC_UNOBSERVED) ent[slot(base, lane, j++)] = (E)((uint32_t)ql | ((uint32_t)c << Tr::kBits));
+        if (c != QSC_UNOBSERVED)
+          ent[slot(base, 64, lane, j++)] = (E)((uint32_t)ql | ((uint32_t)c << Tr::kBits));
       }
     }
-    for (; j < W; ++j) ent[slot(base, lane, j)] = (E)(Tr::kPad << Tr::kBits);
+    for (; j < W; ++j) ent[slot(base, 64, lane, j)] = (E)(Tr::kPad << Tr::kBits);
   }
 }
 
@@ -189,9 +192,9 @@ QSC_API size_t qsc_obs_order_workspace_bytes(int32_t P) {
   return align_up(b) + 3 * align_up((size_t)P * sizeof(int));
 }
 
-QSC_API int qsc_obs_order(const int32_t* cnt, int32_t P, int32_t* perm, void* ws,
+QSC_API int qsc_obs_order(const int32_t* cnt, int32_t P, int32_t Pp, int32_t* perm, void* ws,
                           size_t ws_bytes, void* stream) {
-  if (P < 1 || !cnt || !perm || !ws || ws_bytes < qsc_obs_order_workspace_bytes(P))
+  if (P < 1 || Pp < P || !cnt || !perm || !ws || ws_bytes < qsc_obs_order_workspace_bytes(P))
     return QSC_EINVAL;
   size_t cub_b = 0;
   (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, cub_b, (int*)nullptr, (int*)nullptr,
@@ -208,17 +211,17 @@ QSC_API int qsc_obs_order(const int32_t* cnt, int32_t P, int32_t* perm, void* ws
   hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(cub, cub_b, cnt, keys_out, vals_in,
                                                               perm, P, 0, 32, s);
   if (e != hipSuccess) return (int)e;
-  const int Pp = (int)round_up(P, 64);
   if (Pp > P) {
-    hipLaunchKernelGGL(fill_int_kernel, dim3(1), dim3(64), 0, s, perm + P, Pp - P, -1);
+    hipLaunchKernelGGL(fill_int_kernel, dim3((unsigned)ceil_div(Pp - P, kBlock)), dim3(kBlock), 0,
+                       s, perm + P, Pp - P, -1);
     QSC_CHECK_LAUNCH();
   }
   return QSC_OK;
 }
 
 QSC_API size_t qsc_obs_layout_workspace_bytes(int32_t K, int32_t P, int32_t PT) {
-  const int64_t Pp = round_up(P, 64);
-  const int64_t ns = Pp / 64;
+  const int64_t Pp = round_up(P, PT > 0 ? PT : 64);
+  const int64_t ns = Pp / QSC_SLICE;
   const int64_t nt = ceil_div(Pp, PT > 0 ? PT : 64);
   const int64_t nc = nt * ceil_div(K, 64);
   size_t cb = cub_scan_bytes((int)(ns + 1));
@@ -235,9 +238,8 @@ QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t P
       !codes || !perm || !cnt || !s_width || !s_off || !c_width || !c_off || !desc || !ws ||
       ws_bytes < qsc_obs_layout_workspace_bytes(K, P, PT))
     return QSC_EINVAL;
-  const int Pp = (int)round_up(P, 64);
-  if (Pp % PT) return QSC_EINVAL;
-  const int ns = Pp / 64, nt = Pp / PT, nks = (int)ceil_div(K, 64);
+  const int Pp = (int)round_up(P, PT);  // whole tiles; padding positions carry no entries
+  const int ns = Pp / QSC_SLICE, nt = Pp / PT, nks = (int)ceil_div(K, 64);
   if ((int64_t)nks * 64 * sizeof(int) > 64 * 1024) return QSC_EINVAL;  // LDS counters
   const int wide = (K > 4096 || PT > 4096 || nbins > 15) ? 1 : 0;
   if (wide && ((int64_t)K >= (1 << 24) || (int64_t)PT >= (1 << 24))) return QSC_EINVAL;

@@ -13,16 +13,43 @@
 //           The Adam update of S is fused into the epilogue (no dS round trip through HBM).
 //   C-pass: one lane per frequency bin k of a pixel tile; the lane walks the tile's observed
 //           (pixel, code) list for its k (C-format); C[:,k] and dC[:,k] stay in registers,
-//           S[:,p] is gathered from an LDS copy of the tile.  Per-tile dC partials go to a
-//           slab that qsc_cfinish reduces in a fixed order (bitwise deterministic; no atomics).
+//           S[:,p] is gathered from an LDS copy of the tile.  With few k-slices the list of a
+//           slice is split over several waves (partials combined in LDS in a fixed order).
+//           Per-tile dC partials go to a slab that qsc_cfinish reduces in a fixed order
+//           (bitwise deterministic; no atomics).
+// The per-entry math (lik_grad, qsc_common.cuh) is branch-free so that the four entries of
+// a load chunk are independent instruction streams the scheduler can interleave.
 #include "qsc_common.cuh"
 
 using namespace qsc;
 
 namespace {
 
-constexpr int kBlock = 256;
-constexpr int kWaves = kBlock / 64;
+constexpr int kSBlock = 256;   // S-pass / S-update: 4 waves = 4 slices of QSC_SLICE pixels
+constexpr int kSWaves = kSBlock / 64;
+constexpr int kCBlock = 1024;  // C-pass: 16 waves share one LDS pixel tile
+constexpr int kCWaves = kCBlock / 64;
+constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
+
+// occupancy targets (waves per SIMD) that bound the register allocation of the passes; the
+// rank-16 instances need twice the registers for the S/C row vectors
+#ifndef QSC_SPASS_WAVES
+#define QSC_SPASS_WAVES 8
+#endif
+#ifndef QSC_CPASS_WAVES
+#define QSC_CPASS_WAVES 8
+#endif
+template <int RP, int W>
+struct Occ {
+  static constexpr int v = (RP > 8) ? (W > 4 ? 4 : W) : W;
+};
+
+// LDS row pitch (floats) of an RP-float gathered row: 16-B aligned for ds_read_b128 and, for
+// RP >= 8, not a multiple of 32 B so that random rows spread over all 64 banks
+template <int RP>
+struct Pitch {
+  static constexpr int v = (RP == 4) ? 4 : RP + 4;
+};
 
 template <typename E>
 struct Ent;
@@ -53,54 +80,131 @@ struct Ent<uint32_t> {
   }
 };
 
-// t = sum_r s[r]*c[r] in r order with separate roundings (get_tensor order, bit-identical)
 template <int RP>
-__device__ __forceinline__ float dot_ref(const float* s, const float* c) {
-  float t = __fmul_rn(s[0], c[0]);
+__device__ __forceinline__ float dot_fma(const float* s, const float* c) {
+  float t = s[0] * c[0];
 #pragma unroll
-  for (int r = 1; r < RP; ++r) t = __fadd_rn(t, __fmul_rn(s[r], c[r]));
+  for (int r = 1; r < RP; ++r) t = __builtin_fmaf(s[r], c[r], t);
   return t;
 }
 
+template <int RP>
+__device__ __forceinline__ void lds_vec(const float* base, float (&v)[RP]) {
+#pragma unroll
+  for (int r = 0; r < RP; r += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(base + r);
+    v[r] = x.x;
+    v[r + 1] = x.y;
+    v[r + 2] = x.z;
+    v[r + 3] = x.w;
+  }
+}
+
 struct Scalars {
-  float coef;       // lambda / ||x||  (0 when ||x|| == 0, as torch's norm backward)
+  float coef;  // lambda / ||x||  (0 when ||x|| == 0, as torch's norm backward)
   AdamScalars as;
 };
+
+// Process one 4-entry chunk: `own` is the lane's register vector (S of the pixel or C of the
+// frequency bin), `tab` the LDS table of the other factor indexed by the entry's low bits.
+template <int RP, typename E, int KIND, bool LOG>
+__device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const float (&own)[RP],
+                                      const float* __restrict__ tab,
+                                      const float2* __restrict__ edges, const Lik& lk,
+                                      float (&acc)[RP], float& nll) {
+  using T = Ent<E>;
+  uint32_t e[4];
+  T::unpack(v, e);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int code = (int)(e[u] >> T::kBits);
+    const bool pad = (code == T::kPad);
+    const int idx = pad ? 0 : (int)(e[u] & T::kMask);
+    float o[RP];
+    lds_vec<RP>(tab + idx * Pitch<RP>::v, o);
+    const float t = dot_fma<RP>(own, o);
+    float logP, g;
+    lik_grad<KIND, LOG>(t, pad ? 0 : code, edges, lk, logP, g);
+    g = pad ? 0.0f : g;
+    nll -= pad ? 0.0f : logP;
+#pragma unroll
+    for (int r = 0; r < RP; ++r) acc[r] = __builtin_fmaf(g, o[r], acc[r]);
+#if QSC_ENTRY_BARRIER
+    // one entry at a time: bounded register footprint (8 waves/SIMD) instead of intra-wave ILP
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+  }
+}
+
+// Walk chunks j0, j0+js, j0+2js, ... < j1 of a lane list whose consecutive chunks are `row`
+// V4 units apart (two chunks in flight ahead of the one computed).
+template <int RP, typename E, int KIND, bool LOG>
+__device__ __forceinline__ void walk(const typename Ent<E>::V4* __restrict__ src, int row, int j0,
+                                     int j1, int js, const float (&own)[RP],
+                                     const float* __restrict__ tab,
+                                     const float2* __restrict__ edges, const Lik& lk,
+                                     float (&acc)[RP], float& nll) {
+  using V4 = typename Ent<E>::V4;
+  V4 a = (j0 < j1) ? src[(int64_t)j0 * row] : V4{};
+  V4 b = (j0 + js < j1) ? src[(int64_t)(j0 + js) * row] : V4{};
+  for (int j = j0; j < j1; j += 2 * js) {
+    const V4 c0 = a, c1 = b;
+    if (j + 2 * js < j1) a = src[(int64_t)(j + 2 * js) * row];
+    if (j + 3 * js < j1) b = src[(int64_t)(j + 3 * js) * row];
+    chunk<RP, E, KIND, LOG>(c0, own, tab, edges, lk, acc, nll);
+    if (j + js < j1) chunk<RP, E, KIND, LOG>(c1, own, tab, edges, lk, acc, nll);
+  }
+}
 
 // ---------------------------------------------------------------------------------------
 // S-pass
 // ---------------------------------------------------------------------------------------
-template <int RP, typename E, bool ADAM>
-__global__ void __launch_bounds__(kBlock) spass_kernel(
+template <int RP, typename E, int KIND, bool LOG, bool ADAM>
+__global__ void __launch_bounds__(kSBlock, (Occ<RP, QSC_SPASS_WAVES>::v)) spass_kernel(
     const E* __restrict__ ent, const int* __restrict__ width, const int64_t* __restrict__ off,
-    int nslices, Probit pr, Edges E_, int R, int K, int Pp, float* __restrict__ S,
+    int nslices, Lik lk, Edges E_, int nbins, int R, int K, int Pp, float* __restrict__ S,
     const float* __restrict__ C, float* __restrict__ dS, float* __restrict__ mS,
     float* __restrict__ vS, qsc_adam ad, float lambda_s, qsc_state* __restrict__ st,
     float* __restrict__ part_nll, float* __restrict__ part_nsq) {
   using T = Ent<E>;
+  constexpr int CP = Pitch<RP>::v;
   // all LDS carved from the 16-B aligned dynamic region (no statics ahead of it)
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  Scalars& sc = *reinterpret_cast<Scalars*>(smem);          // 32 B reserved
-  float* Cl = smem + 8;                                      // [K][RP]
-  float2* El = reinterpret_cast<float2*>(Cl + (size_t)K * RP);  // [nbins]
+  Scalars& sc = *reinterpret_cast<Scalars*>(smem);            // 32 B reserved
+  float* Cl = smem + 8;                                        // [K][CP]
+  float2* El = reinterpret_cast<float2*>(Cl + (size_t)K * CP);  // [nbins]
 
   for (int i = threadIdx.x; i < K * RP; i += blockDim.x) {
-    const int k = i / RP, r = i - k * RP;
-    Cl[i] = (r < R) ? C[(int64_t)r * K + k] : 0.0f;
+    const int r = i / K, k = i - r * K;  // coalesced reads of C[r][k]
+    Cl[k * CP + r] = (r < R) ? C[(int64_t)r * K + k] : 0.0f;
   }
-  for (int i = threadIdx.x; i < pr.nbins; i += blockDim.x) El[i] = E_.e[i];
-  if (ADAM && threadIdx.x == 0) {
-    const float nsq = st->normsq_s;
-    const float nrm = sqrtf(nsq);
-    sc.coef = nrm > 0.0f ? lambda_s / nrm : 0.0f;
-    sc.as = adam_scalars(ad, st->step_s + 1);
+  for (int i = threadIdx.x; i < nbins; i += blockDim.x) El[i] = E_.e[i];
+  if (threadIdx.x == 0) {
+    if (ADAM) {
+      const float nrm = sqrtf(st->normsq_s);
+      sc.coef = nrm > 0.0f ? lambda_s / nrm : 0.0f;
+      sc.as = adam_scalars(ad, st->step_s + 1);
+    }
+    if (blockIdx.x == 0) {
+      // book-keeping (fields no block of this kernel reads): see qsc_state
+      int pend = st->pending;
+      if (pend & QSC_PEND_C) st->step_c += 1;
+      pend &= ~QSC_PEND_C;
+      st->pending = pend | QSC_PEND_SNLL | (ADAM ? QSC_PEND_SUPD : 0);
+      st->normsq_s_prev = st->normsq_s;
+      st->iter += 1;
+    }
   }
   __syncthreads();
 
+  // a wave = one slice of QSC_SLICE (32) pixel positions, two lanes per pixel: lane half h
+  // walks the pixel's chunks h, h+2, ...; the halves' partial dS are summed by a lane swap and
+  // each half then updates the rows r with r % 2 == h
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int s = blockIdx.x * kWaves + wave;
+  const int p = lane & (QSC_SLICE - 1), h = lane >> 5;
+  const int s = blockIdx.x * kSWaves + wave;
   if (s >= nslices) return;
-  const int q = s * 64 + lane;
+  const int q = s * QSC_SLICE + p;
 
   float sv[RP], acc[RP];
 #pragma unroll
@@ -109,54 +213,25 @@ __global__ void __launch_bounds__(kBlock) spass_kernel(
     acc[r] = 0.0f;
   }
   float nll = 0.0f;
-
-  const int W4 = width[s] >> 2;
-  const typename T::V4* src = reinterpret_cast<const typename T::V4*>(ent + off[s]) + lane;
-  typename T::V4 cur = W4 > 0 ? src[0] : typename T::V4{};
-  for (int j4 = 0; j4 < W4; ++j4) {
-    typename T::V4 nxt = cur;
-    if (j4 + 1 < W4) nxt = src[(j4 + 1) * 64];
-    uint32_t e[4];
-    T::unpack(cur, e);
+  const typename T::V4* src = reinterpret_cast<const typename T::V4*>(ent + off[s]) + p;
+  walk<RP, E, KIND, LOG>(src, QSC_SLICE, h, width[s] >> 2, 2, sv, Cl, El, lk, acc, nll);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int code = (int)(e[u] >> T::kBits);
-      if (code != T::kPad) {
-        const int k = (int)(e[u] & T::kMask);
-        float c[RP];
-#pragma unroll
-        for (int r = 0; r < RP; r += 4) {
-          const float4 cv = *reinterpret_cast<const float4*>(Cl + k * RP + r);
-          c[r] = cv.x;
-          c[r + 1] = cv.y;
-          c[r + 2] = cv.z;
-          c[r + 3] = cv.w;
-        }
-        const float t = dot_ref<RP>(sv, c);
-        float P, g;
-        entry_grad(t, code, El, pr, P, g);
-        nll -= __logf(P);
-#pragma unroll
-        for (int r = 0; r < RP; ++r) acc[r] = __builtin_fmaf(g, c[r], acc[r]);
-      }
-    }
-    cur = nxt;
-  }
+  for (int r = 0; r < RP; ++r) acc[r] += __shfl_xor(acc[r], 32, 64);
 
   nll = wave_sum(nll);
   if (ADAM) {
     float nsq = 0.0f;
 #pragma unroll
     for (int r = 0; r < RP; ++r) {
-      if (r < R) {
+      if (r < R && (r & 1) == h) {
         const int64_t i = (int64_t)r * Pp + q;
-        float p = sv[r], m = mS[i], v = vS[i];
-        const float g = __fadd_rn(acc[r], __fmul_rn(p, sc.coef));
-        adam_elem(p, m, v, g, ad, sc.as);
-        S[i] = p;
+        float pv = sv[r], m = mS[i], v = vS[i];
+        const float g = __fadd_rn(acc[r], __fmul_rn(pv, sc.coef));
+        adam_elem(pv, m, v, g, ad, sc.as);
+        S[i] = pv;
         mS[i] = m;
         vS[i] = v;
-        nsq = __builtin_fmaf(p, p, nsq);
+        nsq = __builtin_fmaf(pv, pv, nsq);
       }
     }
     nsq = wave_sum(nsq);
@@ -164,7 +239,7 @@ __global__ void __launch_bounds__(kBlock) spass_kernel(
   } else {
 #pragma unroll
     for (int r = 0; r < RP; ++r)
-      if (r < R) dS[(int64_t)r * Pp + q] = acc[r];
+      if (r < R && (r & 1) == h) dS[(int64_t)r * Pp + q] = acc[r];
   }
   if (lane == 0) part_nll[s] = nll;
 }
@@ -172,27 +247,38 @@ __global__ void __launch_bounds__(kBlock) spass_kernel(
 // ---------------------------------------------------------------------------------------
 // C-pass
 // ---------------------------------------------------------------------------------------
-template <int RP, typename E>
-__global__ void __launch_bounds__(kBlock) cpass_kernel(
+template <int RP, typename E, int KIND, bool LOG>
+__global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_kernel(
     const E* __restrict__ ent, const int* __restrict__ width, const int64_t* __restrict__ off,
-    int nks, int PT, Probit pr, Edges E_, int R, int K, int Pp, const float* __restrict__ S,
-    const float* __restrict__ C, float* __restrict__ slab, float* __restrict__ part_nll) {
+    int nks, int split, int PT, Lik lk, Edges E_, int nbins, int R, int K, int Pp,
+    const float* __restrict__ S, const float* __restrict__ C, float* __restrict__ slab,
+    float* __restrict__ part_nll) {
   using T = Ent<E>;
+  constexpr int SP = Pitch<RP>::v;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* Sl = smem;                                          // [PT][RP]
-  float2* El = reinterpret_cast<float2*>(smem + (size_t)PT * RP);  // [nbins]
+  float* Sl = smem;                                              // [PT][SP]
+  float2* El = reinterpret_cast<float2*>(Sl + (size_t)PT * SP);   // [nbins] (<= 254)
+  float* Pl = Sl + (size_t)PT * SP + 2 * 256;                     // split partials [split][R][Kp]
+  float* Nl = Pl + (split > 1 ? (size_t)split * R * nks * 64 : 0);  // [split][nks]
   const int t = blockIdx.x;
   const int64_t q0 = (int64_t)t * PT;
-  for (int i = threadIdx.x; i < PT * RP; i += blockDim.x) {
-    const int r = i / PT, ql = i - r * PT;
-    Sl[ql * RP + r] = (r < R) ? S[(int64_t)r * Pp + q0 + ql] : 0.0f;
+  const int Kp = nks * 64;
+  // stage the pixel tile: one position per thread, R coalesced row reads, 16-B LDS writes
+  for (int ql = threadIdx.x; ql < PT; ql += blockDim.x) {
+    float v[RP];
+#pragma unroll
+    for (int r = 0; r < RP; ++r) v[r] = (r < R) ? S[(int64_t)r * Pp + q0 + ql] : 0.0f;
+#pragma unroll
+    for (int r = 0; r < RP; r += 4)
+      *reinterpret_cast<float4*>(Sl + ql * SP + r) = make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
   }
-  for (int i = threadIdx.x; i < pr.nbins; i += blockDim.x) El[i] = E_.e[i];
+  for (int i = threadIdx.x; i < nbins; i += blockDim.x) El[i] = E_.e[i];
   __syncthreads();
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int Kp = nks * 64;
-  for (int ks = wave; ks < nks; ks += kWaves) {
+  const int units = nks * split;
+  for (int u = wave; u < units; u += kCWaves) {
+    const int ks = u / split, part = u - ks * split;
     const int k = ks * 64 + lane;
     float cv[RP], acc[RP];
 #pragma unroll
@@ -203,66 +289,105 @@ __global__ void __launch_bounds__(kBlock) cpass_kernel(
     float nll = 0.0f;
     const int64_t wi = (int64_t)t * nks + ks;
     const int W4 = width[wi] >> 2;
+    const int j0 = (W4 * part) / split, j1 = (W4 * (part + 1)) / split;
     const typename T::V4* src = reinterpret_cast<const typename T::V4*>(ent + off[wi]) + lane;
-    typename T::V4 cur = W4 > 0 ? src[0] : typename T::V4{};
-    for (int j4 = 0; j4 < W4; ++j4) {
-      typename T::V4 nxt = cur;
-      if (j4 + 1 < W4) nxt = src[(j4 + 1) * 64];
-      uint32_t e[4];
-      T::unpack(cur, e);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int code = (int)(e[u] >> T::kBits);
-        if (code != T::kPad) {
-          const int ql = (int)(e[u] & T::kMask);
-          float s[RP];
-#pragma unroll
-          for (int r = 0; r < RP; r += 4) {
-            const float4 v = *reinterpret_cast<const float4*>(Sl + ql * RP + r);
-            s[r] = v.x;
-            s[r + 1] = v.y;
-            s[r + 2] = v.z;
-            s[r + 3] = v.w;
-          }
-          const float tt = dot_ref<RP>(s, cv);
-          float P, g;
-          entry_grad(tt, code, El, pr, P, g);
-          nll -= __logf(P);
-#pragma unroll
-          for (int r = 0; r < RP; ++r) acc[r] = __builtin_fmaf(g, s[r], acc[r]);
-        }
-      }
-      cur = nxt;
-    }
-#pragma unroll
-    for (int r = 0; r < RP; ++r)
-      if (r < R) slab[((int64_t)t * R + r) * Kp + k] = acc[r];
+    walk<RP, E, KIND, LOG>(src, 64, j0, j1, 1, cv, Sl, El, lk, acc, nll);
     nll = wave_sum(nll);
-    if (lane == 0) part_nll[wi] = nll;
+    if (split == 1) {
+#pragma unroll
+      for (int r = 0; r < RP; ++r)
+        if (r < R) slab[((int64_t)t * R + r) * Kp + k] = acc[r];
+      if (lane == 0) part_nll[wi] = nll;
+    } else {
+#pragma unroll
+      for (int r = 0; r < RP; ++r)
+        if (r < R) Pl[((size_t)part * R + r) * Kp + k] = acc[r];
+      if (lane == 0) Nl[part * nks + ks] = nll;
+    }
   }
+  if (split > 1) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < R * Kp; i += blockDim.x) {
+      float a = Pl[i];
+      for (int p = 1; p < split; ++p) a += Pl[(size_t)p * R * Kp + i];
+      slab[(int64_t)t * R * Kp + i] = a;
+    }
+    for (int ks = threadIdx.x; ks < nks; ks += blockDim.x) {
+      float a = Nl[ks];
+      for (int p = 1; p < split; ++p) a += Nl[p * nks + ks];
+      part_nll[(int64_t)t * nks + ks] = a;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// book-keeping shared by cfinish (block 0) and state_flush: settle a pending S-pass
+// ---------------------------------------------------------------------------------------
+__device__ void settle_s(qsc_state* __restrict__ st, const float* __restrict__ part_nll_s,
+                         const float* __restrict__ part_nsq_s, int nslices, float* hist,
+                         int hist_cap, float* sh) {
+  const int pend = st->pending;  // uniform read (all threads)
+  if (!(pend & (QSC_PEND_SNLL | QSC_PEND_SUPD))) return;
+  float a = 0.0f, b = 0.0f;
+  for (int i = threadIdx.x; i < nslices; i += blockDim.x) {
+    a += part_nll_s[i];
+    if (pend & QSC_PEND_SUPD) b += part_nsq_s[i];
+  }
+  const float nll = block_sum(a, sh);
+  const float nsq = block_sum(b, sh);
+  if (threadIdx.x == 0) {
+    const int it = st->iter - 1;
+    st->nll_s = nll;
+    if (hist && it >= 0 && it < hist_cap) {
+      hist[4 * it + 0] = st->nll_c;
+      hist[4 * it + 1] = nll;
+      hist[4 * it + 2] = st->normsq_c;
+      hist[4 * it + 3] = st->normsq_s_prev;
+    }
+    if (pend & QSC_PEND_SUPD) {
+      st->normsq_s = nsq;
+      st->step_s += 1;
+    }
+    st->pending = pend & ~(QSC_PEND_SNLL | QSC_PEND_SUPD);
+  }
+  __syncthreads();
 }
 
 // ---------------------------------------------------------------------------------------
 // C finish: fixed-order slab reduction (+ fused regulariser / Adam / projection)
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(kBlock) cfinish_kernel(
+__global__ void __launch_bounds__(kFBlock) cfinish_kernel(
     const float* __restrict__ slab, int ntiles, int nks, int R, int K, float* __restrict__ C,
     int mode, float* __restrict__ dC, float* __restrict__ mC, float* __restrict__ vC,
     qsc_adam ad, float lambda_c, const float* __restrict__ normsq_ext,
-    qsc_state* __restrict__ st, const float* __restrict__ part_nll_c, int npart) {
-  __shared__ float red[kWaves][64];
-  __shared__ float shn[kWaves];
+    qsc_state* __restrict__ st, const float* __restrict__ part_nll_c, int npart_c,
+    const float* __restrict__ part_nll_s, const float* __restrict__ part_nsq_s, int nslices,
+    float* __restrict__ hist, int hist_cap) {
+  constexpr int NW = kFBlock / 64;
+  __shared__ float red[NW][64];
+  __shared__ float shn[NW];
   __shared__ Scalars sc;
   const int Kp = nks * 64;
   const int r = blockIdx.x / nks, ks = blockIdx.x - r * nks;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int k = ks * 64 + lane;
 
+  // tile sum: wave w takes tiles w, w+16, ...; eight independent loads in flight
+  const float* col = slab + (int64_t)r * Kp + k;
+  const int64_t tstride = (int64_t)R * Kp;
   float a = 0.0f;
-  for (int t = wave; t < ntiles; t += kWaves) a += slab[((int64_t)t * R + r) * Kp + k];
+  int tt = wave;
+  for (; tt + 7 * NW < ntiles; tt += 8 * NW) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = col[(int64_t)(tt + j * NW) * tstride];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a += v[j];
+  }
+  for (; tt < ntiles; tt += NW) a += col[(int64_t)tt * tstride];
   red[wave][lane] = a;
 
-  float nsq;
+  float nsq = 0.0f;
   if (mode == 1 && normsq_ext == nullptr) {
     // ||C||^2 of the current C, same fixed order in every block
     float s2 = 0.0f;
@@ -281,7 +406,7 @@ __global__ void __launch_bounds__(kBlock) cfinish_kernel(
   if (wave == 0 && k < K) {
     float g = red[0][lane];
 #pragma unroll
-    for (int w = 1; w < kWaves; ++w) g += red[w][lane];
+    for (int w = 1; w < NW; ++w) g += red[w][lane];
     const int64_t i = (int64_t)r * K + k;
     if (mode == 1) {
       float p = C[i], m = mC[i], v = vC[i];
@@ -295,72 +420,64 @@ __global__ void __launch_bounds__(kBlock) cfinish_kernel(
     }
   }
   if (blockIdx.x == 0) {
+    settle_s(st, part_nll_s, part_nsq_s, nslices, hist, hist_cap, shn);
     float s = 0.0f;
-    for (int i = threadIdx.x; i < npart; i += blockDim.x) s += part_nll_c[i];
+    for (int i = threadIdx.x; i < npart_c; i += blockDim.x) s += part_nll_c[i];
     const float tot = block_sum(s, shn);
     if (threadIdx.x == 0) {
       st->nll_c = tot;
-      if (mode == 1) st->normsq_c = nsq;
+      if (mode == 1) {
+        st->normsq_c = nsq;
+        st->pending |= QSC_PEND_C;
+      }
     }
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// S finish: scalars of the S-pass, counters, history
-// ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(1024) sfinish_kernel(const float* __restrict__ part_nll,
-                                                      const float* __restrict__ part_nsq,
-                                                      int nparts, int update_nsq,
-                                                      int c_stepped, int s_stepped,
-                                                      qsc_state* __restrict__ st,
-                                                      float* __restrict__ hist, int hist_cap) {
+__global__ void __launch_bounds__(1024) flush_kernel(qsc_state* __restrict__ st,
+                                                     const float* __restrict__ part_nll_s,
+                                                     const float* __restrict__ part_nsq_s,
+                                                     int nslices, float* __restrict__ hist,
+                                                     int hist_cap) {
   __shared__ float sh[16];
-  float a = 0.0f, b = 0.0f;
-  for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
-    a += part_nll[i];
-    if (update_nsq) b += part_nsq[i];
-  }
-  const float nll = block_sum(a, sh);
-  const float nsq = block_sum(b, sh);
-  if (threadIdx.x == 0) {
-    const int it = st->iter;
-    if (hist && it < hist_cap) {
-      hist[4 * it + 0] = st->nll_c;
-      hist[4 * it + 1] = nll;
-      hist[4 * it + 2] = st->normsq_c;
-      hist[4 * it + 3] = st->normsq_s;
-    }
-    st->nll_s = nll;
-    if (update_nsq) st->normsq_s = nsq;
-    if (c_stepped) st->step_c += 1;
-    if (s_stepped) st->step_s += 1;
-    st->iter = it + 1;
+  settle_s(st, part_nll_s, part_nsq_s, nslices, hist, hist_cap, sh);
+  if (threadIdx.x == 0 && (st->pending & QSC_PEND_C)) {
+    st->step_c += 1;
+    st->pending &= ~QSC_PEND_C;
   }
 }
 
-__global__ void __launch_bounds__(kBlock) adam_kernel(float* __restrict__ x,
-                                                      float* __restrict__ mx,
-                                                      float* __restrict__ vx,
-                                                      const float* __restrict__ g, int64_t n,
-                                                      qsc_adam ad, const int* __restrict__ step,
-                                                      float lambda,
-                                                      const float* __restrict__ normsq) {
+// S update from an all-reduced gradient (K-slab): one thread per position, like the S-pass
+__global__ void __launch_bounds__(kSBlock) supdate_kernel(
+    int nslices, int R, int Pp, float* __restrict__ S, float* __restrict__ mS,
+    float* __restrict__ vS, const float* __restrict__ gsrc, qsc_adam ad, float lambda_s,
+    qsc_state* __restrict__ st, float* __restrict__ part_nsq) {
   __shared__ Scalars sc;
   if (threadIdx.x == 0) {
-    const float nrm = normsq ? sqrtf(*normsq) : 0.0f;
-    sc.coef = (normsq && nrm > 0.0f) ? lambda / nrm : 0.0f;
-    sc.as = adam_scalars(ad, *step + 1);
+    const float nrm = sqrtf(st->normsq_s);
+    sc.coef = nrm > 0.0f ? lambda_s / nrm : 0.0f;
+    sc.as = adam_scalars(ad, st->step_s + 1);
+    if (blockIdx.x == 0) st->pending |= QSC_PEND_SUPD;  // normsq_s / step_s settled later
   }
   __syncthreads();
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float p = x[i], m = mx[i], v = vx[i];
-    const float gg = __fadd_rn(g[i], __fmul_rn(p, sc.coef));
-    adam_elem(p, m, v, gg, ad, sc.as);
-    x[i] = p;
-    mx[i] = m;
-    vx[i] = v;
+  // same lane mapping as the S-pass: 32 positions per wave, rows split by parity
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int s = blockIdx.x * kSWaves + wave;
+  if (s >= nslices) return;
+  const int q = s * QSC_SLICE + (lane & (QSC_SLICE - 1));
+  float nsq = 0.0f;
+  for (int r = lane >> 5; r < R; r += 2) {
+    const int64_t i = (int64_t)r * Pp + q;
+    float p = S[i], m = mS[i], v = vS[i];
+    const float g = __fadd_rn(gsrc[i], __fmul_rn(p, sc.coef));
+    adam_elem(p, m, v, g, ad, sc.as);
+    S[i] = p;
+    mS[i] = m;
+    vS[i] = v;
+    nsq = __builtin_fmaf(p, p, nsq);
   }
+  nsq = wave_sum(nsq);
+  if (lane == 0) part_nsq[s] = nsq;
 }
 
 __global__ void state_init_kernel(qsc_state* st, const double* nsq_part, int nparts) {
@@ -369,13 +486,14 @@ __global__ void state_init_kernel(qsc_state* st, const double* nsq_part, int npa
     for (int i = 0; i < nparts; ++i) s += nsq_part[i];
     qsc_state z{};
     z.normsq_s = (float)s;
+    z.normsq_s_prev = (float)s;
     *st = z;
   }
 }
 
-__global__ void __launch_bounds__(kBlock) nsq_part_kernel(const float* __restrict__ x, int64_t n,
-                                                          double* __restrict__ part) {
-  __shared__ double sh[kWaves];
+__global__ void __launch_bounds__(kSBlock) nsq_part_kernel(const float* __restrict__ x, int64_t n,
+                                                           double* __restrict__ part) {
+  __shared__ double sh[kSWaves];
   double s = 0.0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -384,6 +502,22 @@ __global__ void __launch_bounds__(kBlock) nsq_part_kernel(const float* __restric
   }
   const double r = block_sum(s, sh);
   if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+
+__global__ void __launch_bounds__(1024) sumsq_small_kernel(const float* __restrict__ x, int n,
+                                                           float* __restrict__ out) {
+  __shared__ float sh[16];
+  float s = 0.0f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s = __builtin_fmaf(x[i], x[i], s);
+  const float r = block_sum(s, sh);
+  if (threadIdx.x == 0) *out = r;
+}
+
+__global__ void selftest_erf_kernel(const float* __restrict__ x, int n, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = erff(x[i]);
+  out[n + i] = erf_bf(x[i]);
 }
 
 // ---- workspace layout ----
@@ -406,9 +540,9 @@ PassWs carve(const qsc_obs_desc* d, int R, void* ws) {
   p.cnll = (float*)w;
   w += al((size_t)d->ntiles * d->nks * 4);
   p.snll = (float*)w;
-  w += al((size_t)(d->Pp / 64) * 4);
+  w += al((size_t)(d->Pp / QSC_SLICE) * 4);
   p.snsq = (float*)w;
-  w += al((size_t)(d->Pp / 64) * 4);
+  w += al((size_t)(d->Pp / QSC_SLICE) * 4);
   p.init = (double*)w;
   return p;
 }
@@ -416,7 +550,7 @@ PassWs carve(const qsc_obs_desc* d, int R, void* ws) {
 size_t ws_bytes_for(const qsc_obs_desc* d, int R) {
   const int64_t Kp = (int64_t)d->nks * 64;
   return al((size_t)d->ntiles * R * Kp * 4) + al((size_t)d->ntiles * d->nks * 4) +
-         2 * al((size_t)(d->Pp / 64) * 4) + al(256 * 8);
+         2 * al((size_t)(d->Pp / QSC_SLICE) * 4) + al(256 * 8);
 }
 
 bool desc_ok(const qsc_obs_desc* d) {
@@ -427,9 +561,58 @@ bool desc_ok(const qsc_obs_desc* d) {
 
 int rp_of(int R) { return R <= 4 ? 4 : (R <= 8 ? 8 : 16); }
 
+int split_of(int nks) {
+  int s = 1;
+  while (s * 2 * nks <= kCWaves) s *= 2;
+  return s;
+}
+
+size_t cpass_lds(const qsc_obs_desc* d, int R) {
+  const int RP = rp_of(R), split = split_of(d->nks);
+  size_t b = (size_t)d->PT * (RP == 4 ? 4 : RP + 4) * 4 + 2 * 256 * 4;
+  if (split > 1) b += (size_t)split * R * d->nks * 64 * 4 + (size_t)split * d->nks * 4;
+  return b;
+}
+
 }  // namespace
 
 #define STREAM(s) reinterpret_cast<hipStream_t>(s)
+
+// dispatch over (RP, entry type, likelihood kind, log) for a kernel template K<RP,E,KIND,LOG,...>
+#define QSC_DISPATCH_PASS(LAUNCH)                                                        \
+  do {                                                                                   \
+    if (kind == LIK_ONEBIT) {                                                            \
+      if (d->wide) {                                                                     \
+        if (RP == 4) LAUNCH(4, uint32_t, LIK_ONEBIT, false);                             \
+        else if (RP == 8) LAUNCH(8, uint32_t, LIK_ONEBIT, false);                        \
+        else LAUNCH(16, uint32_t, LIK_ONEBIT, false);                                    \
+      } else {                                                                           \
+        if (RP == 4) LAUNCH(4, uint16_t, LIK_ONEBIT, false);                             \
+        else if (RP == 8) LAUNCH(8, uint16_t, LIK_ONEBIT, false);                        \
+        else LAUNCH(16, uint16_t, LIK_ONEBIT, false);                                    \
+      }                                                                                  \
+    } else if (m->log_model) {                                                           \
+      if (d->wide) {                                                                     \
+        if (RP == 4) LAUNCH(4, uint32_t, LIK_GENERAL, true);                             \
+        else if (RP == 8) LAUNCH(8, uint32_t, LIK_GENERAL, true);                        \
+        else LAUNCH(16, uint32_t, LIK_GENERAL, true);                                    \
+      } else {                                                                           \
+        if (RP == 4) LAUNCH(4, uint16_t, LIK_GENERAL, true);                             \
+        else if (RP == 8) LAUNCH(8, uint16_t, LIK_GENERAL, true);                        \
+        else LAUNCH(16, uint16_t, LIK_GENERAL, true);                                    \
+      }                                                                                  \
+    } else {                                                                             \
+      if (d->wide) {                                                                     \
+        if (RP == 4) LAUNCH(4, uint32_t, LIK_GENERAL, false);                            \
+        else if (RP == 8) LAUNCH(8, uint32_t, LIK_GENERAL, false);                       \
+        else LAUNCH(16, uint32_t, LIK_GENERAL, false);                                   \
+      } else {                                                                           \
+        if (RP == 4) LAUNCH(4, uint16_t, LIK_GENERAL, false);                            \
+        else if (RP == 8) LAUNCH(8, uint16_t, LIK_GENERAL, false);                       \
+        else LAUNCH(16, uint16_t, LIK_GENERAL, false);                                   \
+      }                                                                                  \
+    }                                                                                    \
+  } while (0)
 
 extern "C" {
 
@@ -444,7 +627,7 @@ QSC_API int qsc_state_init(qsc_state* st, const float* S, int32_t R, int32_t Pp,
   double* part = (double*)ws;
   const int nb = 256;
   if (S) {
-    hipLaunchKernelGGL(nsq_part_kernel, dim3(nb), dim3(kBlock), 0, STREAM(stream), S,
+    hipLaunchKernelGGL(nsq_part_kernel, dim3(nb), dim3(kSBlock), 0, STREAM(stream), S,
                        (int64_t)R * Pp, part);
     QSC_CHECK_LAUNCH();
   } else {
@@ -455,53 +638,47 @@ QSC_API int qsc_state_init(qsc_state* st, const float* S, int32_t R, int32_t Pp,
   return QSC_OK;
 }
 
-#define SPASS_LAUNCH(RPV, ET, AD)                                                            \
-  hipLaunchKernelGGL((spass_kernel<RPV, ET, AD>), grid, dim3(kBlock), shm, s,                \
-                     (const ET*)s_entries, s_width, s_off, nslices, pr, E, R, d->K, d->Pp, S, C, \
-                     dS, mS, vS, ad, lambda_s, st, w.snll, w.snsq)
-
 QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
                       const int64_t* s_off, const qsc_model* m, int32_t R, float* S,
                       const float* C, int32_t mode, float* dS, float* mS, float* vS,
                       const qsc_adam* adam, float lambda_s, qsc_state* st, void* ws,
                       size_t ws_bytes, void* stream) {
   if (!desc_ok(d) || !m || m->nbounds - 1 != d->nbins || R < 1 || R > QSC_MAX_R || !S || !C ||
-      !s_width || !s_off || (d->s_entries > 0 && !s_entries) || !ws ||
+      !s_width || !s_off || (d->s_entries > 0 && !s_entries) || !ws || !st ||
       ws_bytes < ws_bytes_for(d, R))
     return QSC_EINVAL;
   if (mode == 0 && !dS) return QSC_EINVAL;
-  if (mode == 1 && (!mS || !vS || !adam || !st)) return QSC_EINVAL;
+  if (mode == 1 && (!mS || !vS || !adam)) return QSC_EINVAL;
   if (mode != 0 && mode != 1) return QSC_EINVAL;
   const int RP = rp_of(R);
-  const size_t shm = 32 + (size_t)d->K * RP * 4 + (size_t)d->nbins * 8;
+  const size_t shm = 32 + (size_t)d->K * (RP == 4 ? 4 : RP + 4) * 4 + (size_t)d->nbins * 8;
   if (shm > 160 * 1024) return QSC_EINVAL;
   PassWs w = carve(d, R, ws);
   Edges E;
   make_edges(m, &E);
-  const Probit pr = make_probit(m);
-  const int nslices = d->Pp / 64;
-  const dim3 grid((unsigned)ceil_div(nslices, kWaves));
+  const Lik lk = make_lik(m);
+  const int kind = lik_kind(m);
+  const int nslices = d->Pp / QSC_SLICE;
+  const dim3 grid((unsigned)ceil_div(nslices, kSWaves));
   qsc_adam ad{};
   if (adam) ad = *adam;
   hipStream_t s = STREAM(stream);
-  const bool A = (mode == 1);
-  if (d->wide) {
-    if (RP == 4) { if (A) SPASS_LAUNCH(4, uint32_t, true); else SPASS_LAUNCH(4, uint32_t, false); }
-    else if (RP == 8) { if (A) SPASS_LAUNCH(8, uint32_t, true); else SPASS_LAUNCH(8, uint32_t, false); }
-    else { if (A) SPASS_LAUNCH(16, uint32_t, true); else SPASS_LAUNCH(16, uint32_t, false); }
-  } else {
-    if (RP == 4) { if (A) SPASS_LAUNCH(4, uint16_t, true); else SPASS_LAUNCH(4, uint16_t, false); }
-    else if (RP == 8) { if (A) SPASS_LAUNCH(8, uint16_t, true); else SPASS_LAUNCH(8, uint16_t, false); }
-    else { if (A) SPASS_LAUNCH(16, uint16_t, true); else SPASS_LAUNCH(16, uint16_t, false); }
-  }
+#define SPASS_LAUNCH(RPV, ET, KD, LG)                                                          \
+  do {                                                                                         \
+    if (mode == 1)                                                                             \
+      hipLaunchKernelGGL((spass_kernel<RPV, ET, KD, LG, true>), grid, dim3(kSBlock), shm, s,   \
+                         (const ET*)s_entries, s_width, s_off, nslices, lk, E, d->nbins, R,    \
+                         d->K, d->Pp, S, C, dS, mS, vS, ad, lambda_s, st, w.snll, w.snsq);     \
+    else                                                                                       \
+      hipLaunchKernelGGL((spass_kernel<RPV, ET, KD, LG, false>), grid, dim3(kSBlock), shm, s,  \
+                         (const ET*)s_entries, s_width, s_off, nslices, lk, E, d->nbins, R,    \
+                         d->K, d->Pp, S, C, dS, mS, vS, ad, lambda_s, st, w.snll, w.snsq);     \
+  } while (0)
+  QSC_DISPATCH_PASS(SPASS_LAUNCH);
+#undef SPASS_LAUNCH
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }
-
-#define CPASS_LAUNCH(RPV, ET)                                                                \
-  hipLaunchKernelGGL((cpass_kernel<RPV, ET>), dim3((unsigned)d->ntiles), dim3(kBlock), shm, s, \
-                     (const ET*)c_entries, c_width, c_off, d->nks, d->PT, pr, E, R, d->K, d->Pp, \
-                     S, C, w.slab, w.cnll)
 
 QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_t* c_width,
                       const int64_t* c_off, const qsc_model* m, int32_t R, const float* S,
@@ -511,30 +688,29 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
       ws_bytes < ws_bytes_for(d, R))
     return QSC_EINVAL;
   const int RP = rp_of(R);
-  const size_t shm = (size_t)d->PT * RP * 4 + (size_t)d->nbins * 8;
+  const size_t shm = cpass_lds(d, R);
   if (shm > 160 * 1024) return QSC_EINVAL;
+  const int split = split_of(d->nks);
   PassWs w = carve(d, R, ws);
   Edges E;
   make_edges(m, &E);
-  const Probit pr = make_probit(m);
+  const Lik lk = make_lik(m);
+  const int kind = lik_kind(m);
   hipStream_t s = STREAM(stream);
-  if (d->wide) {
-    if (RP == 4) CPASS_LAUNCH(4, uint32_t);
-    else if (RP == 8) CPASS_LAUNCH(8, uint32_t);
-    else CPASS_LAUNCH(16, uint32_t);
-  } else {
-    if (RP == 4) CPASS_LAUNCH(4, uint16_t);
-    else if (RP == 8) CPASS_LAUNCH(8, uint16_t);
-    else CPASS_LAUNCH(16, uint16_t);
-  }
+#define CPASS_LAUNCH(RPV, ET, KD, LG)                                                          \
+  hipLaunchKernelGGL((cpass_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles), dim3(kCBlock), \
+                     shm, s, (const ET*)c_entries, c_width, c_off, d->nks, split, d->PT, lk, E, \
+                     d->nbins, R, d->K, d->Pp, S, C, w.slab, w.cnll)
+  QSC_DISPATCH_PASS(CPASS_LAUNCH);
+#undef CPASS_LAUNCH
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }
 
 QSC_API int qsc_cfinish(const qsc_obs_desc* d, int32_t R, float* C, int32_t mode, float* dC,
                         float* mC, float* vC, const qsc_adam* adam, float lambda_c,
-                        const float* normsq_c_ext, qsc_state* st, void* ws, size_t ws_bytes,
-                        void* stream) {
+                        const float* normsq_c_ext, qsc_state* st, float* hist,
+                        int32_t hist_cap, void* ws, size_t ws_bytes, void* stream) {
   if (!desc_ok(d) || R < 1 || R > QSC_MAX_R || !C || !st || !ws || ws_bytes < ws_bytes_for(d, R))
     return QSC_EINVAL;
   if (mode == 0 && !dC) return QSC_EINVAL;
@@ -543,39 +719,51 @@ QSC_API int qsc_cfinish(const qsc_obs_desc* d, int32_t R, float* C, int32_t mode
   PassWs w = carve(d, R, ws);
   qsc_adam ad{};
   if (adam) ad = *adam;
-  hipLaunchKernelGGL(cfinish_kernel, dim3((unsigned)(R * d->nks)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(cfinish_kernel, dim3((unsigned)(R * d->nks)), dim3(kFBlock), 0,
                      STREAM(stream), w.slab, d->ntiles, d->nks, R, d->K, C, mode, dC, mC, vC, ad,
-                     lambda_c, normsq_c_ext, st, w.cnll, d->ntiles * d->nks);
+                     lambda_c, normsq_c_ext, st, w.cnll, d->ntiles * d->nks, w.snll, w.snsq,
+                     d->Pp / QSC_SLICE, hist, hist_cap);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }
 
-QSC_API int qsc_sfinish_ex(const qsc_obs_desc* d, int32_t R, qsc_state* st, float* hist,
-                           int32_t hist_cap, int32_t update_normsq, int32_t c_stepped,
-                           int32_t s_stepped, void* ws, size_t ws_bytes, void* stream) {
+QSC_API int qsc_state_flush(const qsc_obs_desc* d, int32_t R, qsc_state* st, float* hist,
+                            int32_t hist_cap, void* ws, size_t ws_bytes, void* stream) {
   if (!desc_ok(d) || R < 1 || R > QSC_MAX_R || !st || !ws || ws_bytes < ws_bytes_for(d, R))
     return QSC_EINVAL;
   PassWs w = carve(d, R, ws);
-  hipLaunchKernelGGL(sfinish_kernel, dim3(1), dim3(1024), 0, STREAM(stream), w.snll, w.snsq,
-                     d->Pp / 64, update_normsq, c_stepped, s_stepped, st, hist, hist_cap);
+  hipLaunchKernelGGL(flush_kernel, dim3(1), dim3(1024), 0, STREAM(stream), st, w.snll, w.snsq,
+                     d->Pp / QSC_SLICE, hist, hist_cap);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }
 
-QSC_API int qsc_sfinish(const qsc_obs_desc* d, int32_t R, qsc_state* st, float* hist,
-                        int32_t hist_cap, void* ws, size_t ws_bytes, void* stream) {
-  return qsc_sfinish_ex(d, R, st, hist, hist_cap, 1, 1, 1, ws, ws_bytes, stream);
+QSC_API int qsc_supdate(const qsc_obs_desc* d, int32_t R, float* S, float* mS, float* vS,
+                        const float* g, const qsc_adam* adam, float lambda_s, qsc_state* st,
+                        void* ws, size_t ws_bytes, void* stream) {
+  if (!desc_ok(d) || R < 1 || R > QSC_MAX_R || !S || !mS || !vS || !g || !adam || !st || !ws ||
+      ws_bytes < ws_bytes_for(d, R))
+    return QSC_EINVAL;
+  PassWs w = carve(d, R, ws);
+  const int nslices = d->Pp / QSC_SLICE;
+  hipLaunchKernelGGL(supdate_kernel, dim3((unsigned)ceil_div(nslices, kSWaves)), dim3(kSBlock), 0,
+                     STREAM(stream), nslices, R, d->Pp, S, mS, vS, g, *adam, lambda_s, st, w.snsq);
+  QSC_CHECK_LAUNCH();
+  return QSC_OK;
 }
 
-QSC_API int qsc_adam_step(float* x, float* mx, float* vx, const float* g, int64_t n,
-                          const qsc_adam* adam, const int32_t* step, float lambda,
-                          const float* normsq, void* stream) {
-  if (n < 0 || (n > 0 && (!x || !mx || !vx || !g)) || !adam || !step) return QSC_EINVAL;
+QSC_API int qsc_sumsq_small(const float* x, int32_t n, float* out, void* stream) {
+  if (n < 0 || !x || !out) return QSC_EINVAL;
+  hipLaunchKernelGGL(sumsq_small_kernel, dim3(1), dim3(1024), 0, STREAM(stream), x, n, out);
+  QSC_CHECK_LAUNCH();
+  return QSC_OK;
+}
+
+QSC_API int qsc_selftest_erf(const float* x, int32_t n, float* out, void* stream) {
+  if (n < 0 || !x || !out) return QSC_EINVAL;
   if (n == 0) return QSC_OK;
-  const int64_t g0 = ceil_div(n, kBlock);
-  const unsigned grid = (unsigned)(g0 > 8192 ? 8192 : g0);
-  hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(kBlock), 0, STREAM(stream), x, mx, vx, g, n,
-                     *adam, step, lambda, normsq);
+  hipLaunchKernelGGL(selftest_erf_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0,
+                     STREAM(stream), x, n, out);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }

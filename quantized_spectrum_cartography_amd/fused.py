@@ -5,9 +5,10 @@ differentiates:
   C-step:  qsc_cpass (per-tile dC partials)  ->  qsc_cfinish (fixed-order reduction,
            + lambda_c C/||C||, Adam, C[C<0] = 0)               qmc/qmc.ipynb :562-579
   S-step:  qsc_spass (dS in registers, + lambda_s S/||S||, Adam fused in the epilogue)
-           ->  qsc_sfinish (scalars, step counters)             qmc/qmc.ipynb :622-634
-All scalars (step counters, ||S||^2, NLLs) stay on the device, so an iteration is four
-kernel launches with no host synchronisation and can be captured in one hipGraph.
+                                                                qmc/qmc.ipynb :622-634
+Scalars (step counters, ||S||^2, NLLs, the cost history) stay on the device and their
+book-keeping rides on those same kernels (qsc_state protocol in include/qsc.h), so an outer
+iteration is three launches with no host synchronisation and is captured in one hipGraph.
 """
 import torch
 
@@ -40,6 +41,9 @@ class PassEngine:
     def read_state(self):
         return _lib.read_state(self.state)
 
+    def field(self, name):
+        return _lib.state_field(self.state, name)
+
     # ---- passes -------------------------------------------------------------------------
     def cpass(self, S_pos, C):
         o = self.obs
@@ -47,10 +51,13 @@ class PassEngine:
                   o.model, self.R, _lib.ptr(S_pos), _lib.ptr(C), _lib.ptr(self.ws), self.ws.numel(),
                   _lib.stream())
 
-    def cfinish(self, C, mode, dC=None, mC=None, vC=None, adam=None, lambda_c=0.0, normsq_ext=None):
+    def cfinish(self, C, mode, dC=None, mC=None, vC=None, adam=None, lambda_c=0.0,
+                normsq_ext=None, record=True):
+        hist, cap = (self.hist, self.hist_cap) if (record and self.hist_cap) else (None, 0)
         _lib.call("qsc_cfinish", self.obs.desc, self.R, _lib.ptr(C), int(mode), _lib.ptr(dC),
                   _lib.ptr(mC), _lib.ptr(vC), adam, float(lambda_c), _lib.ptr(normsq_ext),
-                  _lib.ptr(self.state), _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
+                  _lib.ptr(self.state), _lib.ptr(hist), cap, _lib.ptr(self.ws), self.ws.numel(),
+                  _lib.stream())
 
     def spass(self, S_pos, C, mode, dS=None, mS=None, vS=None, adam=None, lambda_s=0.0):
         o = self.obs
@@ -59,10 +66,19 @@ class PassEngine:
                   _lib.ptr(mS), _lib.ptr(vS), adam, float(lambda_s), _lib.ptr(self.state),
                   _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
 
-    def sfinish(self, update_normsq=True, c_stepped=True, s_stepped=True):
-        _lib.call("qsc_sfinish_ex", self.obs.desc, self.R, _lib.ptr(self.state), _lib.ptr(self.hist),
-                  self.hist_cap, int(update_normsq), int(c_stepped), int(s_stepped),
-                  _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
+    def supdate(self, S_pos, mS, vS, g, adam, lambda_s):
+        _lib.call("qsc_supdate", self.obs.desc, self.R, _lib.ptr(S_pos), _lib.ptr(mS), _lib.ptr(vS),
+                  _lib.ptr(g), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),
+                  self.ws.numel(), _lib.stream())
+
+    def sumsq(self, x, out):
+        """out[0] = ||x||^2 (fixed order, one workgroup; for small vectors such as C)."""
+        _lib.call("qsc_sumsq_small", _lib.ptr(x), x.numel(), _lib.ptr(out), _lib.stream())
+
+    def flush(self, record=True):
+        hist, cap = (self.hist, self.hist_cap) if (record and self.hist_cap) else (None, 0)
+        _lib.call("qsc_state_flush", self.obs.desc, self.R, _lib.ptr(self.state), _lib.ptr(hist),
+                  cap, _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
 
     # ---- composite ----------------------------------------------------------------------
     def nll_grad(self, S_pos, C, need_dS=True, need_dC=True):
@@ -70,15 +86,15 @@ class PassEngine:
         R, Pp = self.R, self.obs.Pp
         dS = torch.empty((R, Pp), dtype=torch.float32, device=S_pos.device) if need_dS else None
         dC = torch.empty_like(C) if need_dC else None
-        if need_dC:
+        if need_dC or not need_dS:
             self.cpass(S_pos, C)
-            self.cfinish(C, 0, dC=dC)
+            self.cfinish(C, 0, dC=dC if need_dC else torch.empty_like(C), record=False)
         if need_dS:
             self.spass(S_pos, C, 0, dS=dS)
-            self.sfinish(update_normsq=False, c_stepped=False, s_stepped=False)
-            nll = self.state[28:32].view(torch.float32)[0].clone()  # nll_s
+            self.flush(record=False)
+            nll = self.field("nll_s").clone()[0]
         else:
-            nll = self.state[24:28].view(torch.float32)[0].clone()  # nll_c
+            nll = self.field("nll_c").clone()[0]
         return nll, dS, dC
 
 

@@ -20,11 +20,7 @@ def default_tile(P, R, K):
     cap -= cap % 64
     want = max(64, -(-Pp // 512))
     want = -(-want // 64) * 64
-    PT = min(want, cap)
-    # PT must divide Pp
-    while Pp % PT:
-        PT -= 64
-    return PT
+    return min(want, cap)
 
 
 class Observations:
@@ -39,12 +35,15 @@ class Observations:
     """
 
     def __init__(self, Y, Wx, bin_boundaries, noise_std, offset=0.0, log_model=False, perm=None,
-                 tile=None, R_hint=8):
+                 tile=None, R_hint=8, count_hook=None):
         K = Y.shape[0]
         I, J = Y.shape[-2], Y.shape[-1]
         P = I * J
         self.K, self.I, self.J, self.P = K, I, J, P
-        self.Pp = -(-P // 64) * 64
+        PT = int(tile or default_tile(P, R_hint, K))
+        if PT < 64 or PT % 64:
+            raise ValueError("tile must be a positive multiple of 64")
+        self.Pp = -(-P // PT) * PT  # whole tiles; padding positions carry no observations
         self.model = _lib.make_model(bin_boundaries, noise_std, offset if log_model else 0.0,
                                      log_model)
         self.log_model = bool(log_model)
@@ -73,18 +72,19 @@ class Observations:
         _lib.call("qsc_obs_count", _lib.ptr(codes), K, P, _lib.ptr(cnt), s)
         self.counts = cnt
         if perm is None:
+            # count_hook (e.g. an all-reduce over K-slab ranks) makes the pixel order a function
+            # of the global counts, so every rank lays S out identically
+            order_cnt = count_hook(cnt.clone()) if count_hook is not None else cnt
             perm = torch.empty(self.Pp, dtype=torch.int32, device=dev)
             ws = _ws(_lib.lib().qsc_obs_order_workspace_bytes(P), dev)
-            _lib.call("qsc_obs_order", _lib.ptr(cnt), P, _lib.ptr(perm), _lib.ptr(ws), ws.numel(), s)
+            _lib.call("qsc_obs_order", _lib.ptr(order_cnt), P, self.Pp, _lib.ptr(perm), _lib.ptr(ws),
+                      ws.numel(), _lib.stream())
         else:
             perm = _dev(perm.to(torch.int32))
             if perm.numel() != self.Pp:
                 raise ValueError("perm must have Pp = %d entries" % self.Pp)
         self.perm = perm
-        PT = tile or default_tile(P, R_hint, K)
-        if PT % 64 or self.Pp % PT:
-            raise ValueError("tile must be a multiple of 64 dividing Pp=%d" % self.Pp)
-        ns, nt, nks = self.Pp // 64, self.Pp // PT, -(-K // 64)
+        ns, nt, nks = self.Pp // _lib.QSC_SLICE, self.Pp // PT, -(-K // 64)
         self.s_width = torch.empty(ns, dtype=torch.int32, device=dev)
         self.s_off = torch.empty(ns + 1, dtype=torch.int64, device=dev)
         self.c_width = torch.empty(nt * nks, dtype=torch.int32, device=dev)

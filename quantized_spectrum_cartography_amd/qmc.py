@@ -70,7 +70,6 @@ class FreeSSolver:
     def s_step(self):
         e = self.engine
         e.spass(self.S, self.C, 1, mS=self.mS, vS=self.vS, adam=self.adam_s, lambda_s=self.lambda_s)
-        e.sfinish(update_normsq=True, c_stepped=True, s_stepped=True)
 
     def iteration(self):
         self.c_step()
@@ -109,6 +108,7 @@ class FreeSSolver:
         return self.obs.to_pixels(self.S).reshape(self.R, 1, self.obs.I, self.obs.J)
 
     def history(self):
+        self.engine.flush()  # settle the last S-pass (its history row)
         st = self.state()
         n = min(int(st["iter"]), self.engine.hist_cap)
         h = self.engine.hist[: 4 * n].view(n, 4).double().cpu()
@@ -189,12 +189,11 @@ def _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c
     eng.init_state(S_pos)
     dS_pos = torch.empty_like(S_pos)
     costs_c, costs_s, nmse = [], [], []
-    step_c = 0
 
     def nll_of(S_cand):
         Sp = obs.to_positions(S_cand.reshape(R, -1))
         eng.spass(Sp, C, 0, dS=dS_pos)
-        eng.sfinish(update_normsq=False, c_stepped=False, s_stepped=False)
+        eng.flush(record=False)
         return eng.read_state()["nll_s"]
 
     for i in range(max_iter):
@@ -203,10 +202,8 @@ def _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c
         eng.cpass(S_pos, C)
         eng.cfinish(C, 1, mC=mC, vC=vC, adam=adam_c, lambda_c=lambda_c)
         st = eng.read_state()
-        costs_c.append(st["nll_c"] + lambda_c * math.sqrt(nsq_c) + lambda_s * float(torch.norm(Z)))
-        # cfinish read step_c + 1; advance it (sfinish also reduces nothing new here)
-        eng.sfinish(update_normsq=False, c_stepped=True, s_stepped=False)
-        step_c += 1
+        costs_c.append(st["nll_c"] + lambda_c * math.sqrt(nsq_c) + lambda_s * float(torch.norm(Z.detach())))
+        # (cfinish left step_c += 1 pending; the next S-pass applies it)
         # ---- one-time random restart of Z (:590-619) ----
         if restart and i == 1:
             best = float("inf")
@@ -233,14 +230,14 @@ def _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c
         S = generator(Z).reshape(R, 1, I, J)
         S_pos = obs.to_positions(S.detach().reshape(R, -1))
         eng.spass(S_pos, C, 0, dS=dS_pos)
-        eng.sfinish(update_normsq=False, c_stepped=False, s_stepped=False)
+        eng.flush(record=False)
         dS = obs.to_pixels(dS_pos).reshape(R, 1, I, J)
         reg = lambda_s * torch.norm(Z, "fro")
         surrogate = (S * dS).sum() + reg
         surrogate.backward()
         optS.step()
         st = eng.read_state()
-        costs_s.append(st["nll_s"] + lambda_c * float(torch.norm(C)) + float(reg))
+        costs_s.append(st["nll_s"] + lambda_c * float(torch.norm(C)) + float(reg.detach()))
         if T_true is not None and nmse_every and (i + 1) % nmse_every == 0:
             nmse.append(map_nmse(S.detach(), C, T_true))
         if callback is not None:

@@ -40,6 +40,39 @@ def onebit_problem(I, J, K, R, f=0.1, seed=20260, device="cuda", keep_T=True):
     return out
 
 
+def kslab_onebit_problem(I, J, K_local, R, rank, world, dist=None, f=0.1, seed=20260,
+                         device="cuda"):
+    """One rank's K-slab of a global one-bit problem with K_local * world frequency bins.
+
+    S_true and S0 are common to all ranks (same seed); C_true / C0 columns, the noise and the
+    mask are drawn per slab.  The quantizer (thr = mean of the slabs' medians, sigma from the
+    global min/max) is agreed over `dist` so that all slabs share one probit model."""
+    g = torch.Generator().manual_seed(seed)
+    S_true = torch.rand(R, 1, I, J, generator=g)
+    S0 = 0.5 * torch.rand(R, 1, I, J, generator=g)
+    gl = torch.Generator().manual_seed(seed + 1000 + rank)
+    C_true = torch.rand(R, K_local, generator=gl)
+    C0 = 0.5 * torch.rand(R, K_local, generator=gl)
+    T = _model.get_tensor(S_true.to(device), C_true.to(device))
+    stats = torch.tensor([float(T.median()), -float(T.min()), float(T.max())], dtype=torch.float64,
+                         device=device)
+    if dist is not None and world > 1:
+        med = stats[:1].clone()
+        dist.all_reduce(med)
+        mx = stats[1:].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        stats = torch.cat([med / world, mx])
+    thr, tmin, tmax = float(stats[0]), -float(stats[1]), float(stats[2])
+    sigma = (tmax - tmin) / 4
+    b = torch.tensor([0.0, thr, tmax])
+    noise = torch.randn(T.shape, generator=gl)
+    Y = _model.quantize(T, sigma, b, noise=noise).unsqueeze(1)
+    del noise
+    Wx = torch.bernoulli(torch.full((K_local, 1, I, J), f), generator=gl)
+    return dict(S_true=S_true, C_true=C_true, b=b, sigma=sigma, Y=Y, Wx=Wx, S0=S0, C0=C0,
+                log_model=False, offset=0.0, thr=thr, T_true=T)
+
+
 CONFIGS = {
     # name: (I, J, K, R)   BASELINE.json configs
     "c2": (256, 256, 64, 4),

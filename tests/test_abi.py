@@ -19,9 +19,9 @@ def libpath():
 
 def test_header_parses_all_entry_points():
     h = _lib.parse_header()
-    for name in ("qsc_spass", "qsc_cpass", "qsc_cfinish", "qsc_sfinish", "qsc_quantize",
+    for name in ("qsc_spass", "qsc_cpass", "qsc_cfinish", "qsc_quantize",
                  "qsc_prob_probit", "qsc_reconstruct", "qsc_gram", "qsc_chol_solve",
-                 "qsc_obs_layout", "qsc_adam_step"):
+                 "qsc_obs_layout", "qsc_supdate", "qsc_state_flush"):
         assert name in h
     assert len(h) >= 30
 
@@ -78,3 +78,16 @@ def test_product_fails_loudly_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(_lib.QscError):
         qm.get_tensor(torch.rand(2, 1, 4, 4), torch.rand(2, 3))
+
+
+def test_host_constants_match_header():
+    """Host-side buffer sizing uses these constants (e.g. s_width has Pp / QSC_SLICE entries):
+    they must equal the header's #defines."""
+    import re
+    src = open(_lib.HEADER).read()
+    defs = dict(re.findall(r"#define\s+(QSC_[A-Z0-9_]+)\s+(0x[0-9A-Fa-f]+|\d+)\b", src))
+    assert int(defs["QSC_SLICE"]) == _lib.QSC_SLICE
+    assert int(defs["QSC_MAX_R"]) == _lib.QSC_MAX_R
+    assert int(defs["QSC_MAX_BOUNDS"]) == _lib.QSC_MAX_BOUNDS
+    assert int(defs["QSC_EINVAL"]) == _lib.QSC_EINVAL
+    assert int(defs["QSC_UNOBSERVED"], 0) == _lib.UNOBSERVED

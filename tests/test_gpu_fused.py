@@ -160,31 +160,53 @@ def test_mat_fixture_onebit_solve(golden):
     b = torch.tensor([0.0, 0.0045, float(g["T_true"].max())])
     sigma = 0.02
     gen = torch.Generator().manual_seed(5)
-    S0 = 0.5 * torch.rand(2, 1, 51, 51, generator=gen)
-    C0 = 0.5 * torch.rand(2, K, generator=gen)
+    # start inside the data range (max T_true = 0.074) so that P(Y | T_hat) stays > 0
+    S0 = 0.1 * torch.rand(2, 1, 51, 51, generator=gen)
+    C0 = 0.1 * torch.rand(2, K, generator=gen)
     res = qmc.solve(Y, Wx, b, sigma, S_init=S0, C_init=C0, max_iter=5)
     ref = osolver.free_s_solve(S0, C0, Y, Wx, b, sigma, n_iter=5)
     assert rel_fro(res.S.cpu().numpy(), ref["S"].numpy()) < 1e-5
     assert rel_fro(res.C.cpu().numpy(), ref["C"].numpy()) < 1e-5
 
 
-def test_generator_solver_runs_and_decreases_cost():
+def test_generator_solver_vs_oracle():
+    """GAN path (qmc/qmc.ipynb :541-634, config-1 setting: log model, 4 log bins, f = 0.1,
+    sigma = 5, zero C, Z ~ N(0,1), random restart at i == 1) vs the oracle's loop with the same
+    random-init Generator256.  The generator is plain torch on both sides (CPU vs MIOpen conv
+    numerics differ in the last bits), so the tolerance is 1e-4."""
+    import copy
     from quantized_spectrum_cartography_amd import nets, qmc
     from quantized_spectrum_cartography_amd.utils import LOG_OFFSET_4, QUANTIZATION_BOUNDARIES_4_BINS_LOG
     torch.manual_seed(0)
     R, K = 2, 64
-    gen = nets.Generator256().cuda().eval()
+    gen = nets.Generator256().eval()
+    # random-init weights map every Z to S ~ 0.5, so the restart candidates' criteria tie to
+    # within an ulp and the argmin would be decided by rounding; steeper layers make
+    # the candidates distinguishable (the selection logic is what this test checks)
+    with torch.no_grad():
+        for mod in gen.modules():
+            if isinstance(mod, (torch.nn.ConvTranspose2d, torch.nn.Conv2d)):
+                mod.weight.mul_(3.0)  # S in ~(0.05, 0.97), strongly Z-dependent
+                mod.bias.zero_()
     S_true = torch.rand(R, 1, 51, 51) ** 4 * 0.2
     C_true = torch.rand(R, K)
     Tt = ro.get_tensor(S_true, C_true)
-    Y = ro.quantize(Tt, 5.0, torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG), offset=LOG_OFFSET_4,
-                    log_model=True).unsqueeze(1)
+    b = torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG)
+    Y = ro.quantize(Tt, 5.0, b, offset=LOG_OFFSET_4, log_model=True).unsqueeze(1)
     Wx = torch.bernoulli(torch.full((K, 1, 51, 51), 0.1))
-    res = qmc.solve(Y, Wx, torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG), 5.0, R=R,
-                    offset=LOG_OFFSET_4, log_model=True, generator=gen, Z_init=torch.randn(R, 256),
-                    C_init=torch.zeros(R, K), max_iter=6, restart=True, restart_samples=(5, 5))
+    Z0 = torch.randn(R, 256)
+    torch.manual_seed(99)
+    ref = osolver.generator_solve(copy.deepcopy(gen), Z0, torch.zeros(R, K), Y, Wx, b, 5.0,
+                                  LOG_OFFSET_4, True, n_iter=4, restart=True,
+                                  restart_samples=(5, 5))
+    torch.manual_seed(99)
+    res = qmc.solve(Y, Wx, b, 5.0, R=R, offset=LOG_OFFSET_4, log_model=True,
+                    generator=copy.deepcopy(gen).cuda(), Z_init=Z0, C_init=torch.zeros(R, K),
+                    max_iter=4, restart=True, restart_samples=(5, 5))
     assert res.S.shape == (R, 1, 51, 51)
-    assert np.all(np.isfinite(res.costs_s)) and res.costs_s[-1] < res.costs_s[0]
+    assert rel_fro(res.Z.cpu().numpy(), ref["Z"].numpy()) < 1e-4
+    assert rel_fro(res.C.cpu().numpy(), ref["C"].numpy()) < 1e-4
+    assert np.allclose(res.costs_s, ref["costs_s"], rtol=1e-4)
 
 
 def test_dip_solver_256():
