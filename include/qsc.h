@@ -101,6 +101,9 @@ typedef struct qsc_state {
  *     idx = s_off[s] + (j/4)*128 + l*4 + (j%4);  value = k | code << KBITS  (code PAD = pad)
  *     (the S-pass gives each pixel two lanes, which take alternate 4-entry chunks) */
 #define QSC_SLICE 32
+/* Both entry arrays end with QSC_ENTRY_TAIL pad entries (counted in s_entries / c_entries) so
+ * that the passes may issue their read-ahead loads without bounds branches. */
+#define QSC_ENTRY_TAIL 256
 /*
  *  C-format ("frequency slices" per pixel tile): tile t (PT positions), k-slice ks (64 k's),
  *     lane l (k = 64*ks + l), entry j < c_width[t*nks+ks]:
@@ -262,7 +265,7 @@ QSC_API int qsc_supdate(const qsc_obs_desc* d, int32_t R, float* S, float* mS, f
                         void* ws, size_t ws_bytes, void* stream);
 /* ||x||^2 into *out (fp32, fixed order), e.g. the local ||C_slab||^2 before an all-reduce */
 QSC_API int qsc_sumsq_small(const float* x, int32_t n, float* out, void* stream);
-/* diagnostics: out[0..n) = ocml erff(x), out[n..2n) = the branch-free erf of the passes */
+/* diagnostics: out[0..n) = ocml erff(x), out[n..2n) = the erf of the fused passes (erf_fast) */
 QSC_API int qsc_selftest_erf(const float* x, int32_t n, float* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------

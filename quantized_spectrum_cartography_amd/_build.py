@@ -17,9 +17,10 @@ SOURCES = ["qsc_ops.hip", "qsc_obs.hip", "qsc_pass.hip", "qsc_gram.hip"]
 ARCH = os.environ.get("QSC_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: hipcc contracts a*b+c into FMA by default, which would change the
 # reference's separately rounded products and sums (get_tensor, quantize); FMAs that are
-# wanted are written explicitly with __builtin_fmaf.
+# wanted are written explicitly with __builtin_fmaf.  -fno-slp-vectorize: pairing scalar f32
+# lanes into v_pk_* ops costs a v_mov per operand and s_nop hazards in the fused passes.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall",
-          "-Wno-unused-function", "-ffp-contract=off"]
+          "-Wno-unused-function", "-ffp-contract=off", "-fno-slp-vectorize"]
 
 
 def _hipcc():
@@ -39,9 +40,13 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force=False, verbose=True):
-    """Compile every HIP source for gfx950 and link libqsc_hip.so (parallel, one hipcc per file)."""
-    if not force and not _stale():
+def build(force=False, verbose=True, out=None, extra_flags=()):
+    """Compile every HIP source for gfx950 and link libqsc_hip.so (parallel, one hipcc per file).
+
+    `out` / `extra_flags` produce a variant library (e.g. -DQSC_SPASS_WAVES=4 for tuning runs,
+    loaded through QSC_LIB_PATH); the default build is always the in-tree LIB_PATH."""
+    lib_path = out or LIB_PATH
+    if out is None and not force and not _stale():
         return LIB_PATH
     hipcc = _hipcc()
     tmp = tempfile.mkdtemp(prefix="qsc_build_")
@@ -51,7 +56,7 @@ def build(force=False, verbose=True):
         for src in SOURCES:
             obj = os.path.join(tmp, src.replace(".hip", ".o"))
             objs.append(obj)
-            cmd = [hipcc] + CFLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
+            cmd = [hipcc] + CFLAGS + list(extra_flags) + ["-c", os.path.join(CSRC, src), "-o", obj]
             procs.append((src, cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE,
                                                      stderr=subprocess.STDOUT)))
         failed = []
@@ -64,15 +69,15 @@ def build(force=False, verbose=True):
         if failed:
             msg = "\n".join("---- %s ----\n%s" % f for f in failed)
             raise RuntimeError("hipcc failed:\n" + msg)
-        out_tmp = LIB_PATH + ".tmp"
+        out_tmp = lib_path + ".tmp"
         cmd = [hipcc, "-shared", "-fPIC", "--offload-arch=" + ARCH] + objs + ["-o", out_tmp]
         subprocess.check_call(cmd)
-        os.replace(out_tmp, LIB_PATH)
+        os.replace(out_tmp, lib_path)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     if verbose:
-        print("built", LIB_PATH)
-    return LIB_PATH
+        print("built", lib_path)
+    return lib_path
 
 
 if __name__ == "__main__":

@@ -18,6 +18,7 @@ HEADER = os.path.join(os.path.dirname(_build.PKG_DIR), "include", "qsc.h")
 QSC_MAX_BOUNDS = 256
 QSC_MAX_R = 16
 QSC_SLICE = 32  # S-format slice (pixel positions per list group), include/qsc.h
+QSC_ENTRY_TAIL = 256  # pad entries after the last list (read-ahead tail), include/qsc.h
 QSC_EINVAL = 100000
 UNOBSERVED = 0xFF
 

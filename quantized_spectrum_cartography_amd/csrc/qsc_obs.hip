@@ -97,6 +97,13 @@ __device__ __forceinline__ int64_t slot(int64_t base, int lanes, int lane, int j
   return base + (int64_t)(j >> 2) * (lanes * 4) + lane * 4 + (j & 3);
 }
 
+// pad entries after the last list (read-ahead tail, QSC_ENTRY_TAIL)
+template <typename E>
+__global__ void tail_fill_kernel(E* __restrict__ ent, int64_t start, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) ent[start + i] = (E)(EntryTraits<E>::kPad << EntryTraits<E>::kBits);
+}
+
 template <typename E>
 __global__ void __launch_bounds__(kBlock) s_fill_kernel(const uint8_t* __restrict__ codes,
                                                         const int* __restrict__ perm, int K,
@@ -284,8 +291,8 @@ QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t P
   desc->nks = nks;
   desc->wide = wide;
   desc->nbins = nbins;
-  desc->s_entries = host_tot[0];
-  desc->c_entries = host_tot[1];
+  desc->s_entries = host_tot[0] + QSC_ENTRY_TAIL;
+  desc->c_entries = host_tot[1] + QSC_ENTRY_TAIL;
   desc->nnz = host_tot[2];
   return QSC_OK;
 }
@@ -293,10 +300,16 @@ QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t P
 QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* d, const int32_t* perm,
                          const int32_t* s_width, const int64_t* s_off, const int32_t* c_width,
                          const int64_t* c_off, void* s_entries, void* c_entries, void* stream) {
-  if (!d || !codes || !perm || !s_width || !s_off || !c_width || !c_off) return QSC_EINVAL;
-  if ((d->s_entries > 0 && !s_entries) || (d->c_entries > 0 && !c_entries)) return QSC_EINVAL;
+  if (!d || !codes || !perm || !s_width || !s_off || !c_width || !c_off || !s_entries ||
+      !c_entries || d->s_entries < QSC_ENTRY_TAIL || d->c_entries < QSC_ENTRY_TAIL)
+    return QSC_EINVAL;
   hipStream_t s = STREAM(stream);
+  const dim3 tg((QSC_ENTRY_TAIL + kBlock - 1) / kBlock), tb(kBlock);
   if (d->wide) {
+    hipLaunchKernelGGL(tail_fill_kernel<uint32_t>, tg, tb, 0, s, (uint32_t*)s_entries,
+                       d->s_entries - QSC_ENTRY_TAIL, QSC_ENTRY_TAIL);
+    hipLaunchKernelGGL(tail_fill_kernel<uint32_t>, tg, tb, 0, s, (uint32_t*)c_entries,
+                       d->c_entries - QSC_ENTRY_TAIL, QSC_ENTRY_TAIL);
     hipLaunchKernelGGL(s_fill_kernel<uint32_t>, dim3((unsigned)ceil_div(d->Pp, kBlock)),
                        dim3(kBlock), 0, s, codes, perm, d->K, d->P, d->Pp, s_width, s_off,
                        (uint32_t*)s_entries);
@@ -305,6 +318,10 @@ QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* d, const int3
                        codes, perm, d->K, d->P, d->PT, d->nks, c_width, c_off,
                        (uint32_t*)c_entries);
   } else {
+    hipLaunchKernelGGL(tail_fill_kernel<uint16_t>, tg, tb, 0, s, (uint16_t*)s_entries,
+                       d->s_entries - QSC_ENTRY_TAIL, QSC_ENTRY_TAIL);
+    hipLaunchKernelGGL(tail_fill_kernel<uint16_t>, tg, tb, 0, s, (uint16_t*)c_entries,
+                       d->c_entries - QSC_ENTRY_TAIL, QSC_ENTRY_TAIL);
     hipLaunchKernelGGL(s_fill_kernel<uint16_t>, dim3((unsigned)ceil_div(d->Pp, kBlock)),
                        dim3(kBlock), 0, s, codes, perm, d->K, d->P, d->Pp, s_width, s_off,
                        (uint16_t*)s_entries);

@@ -34,10 +34,10 @@ constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 // occupancy targets (waves per SIMD) that bound the register allocation of the passes; the
 // rank-16 instances need twice the registers for the S/C row vectors
 #ifndef QSC_SPASS_WAVES
-#define QSC_SPASS_WAVES 8
+#define QSC_SPASS_WAVES 4
 #endif
 #ifndef QSC_CPASS_WAVES
-#define QSC_CPASS_WAVES 8
+#define QSC_CPASS_WAVES 4
 #endif
 template <int RP, int W>
 struct Occ {
@@ -123,10 +123,10 @@ __device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const float 
     float o[RP];
     lds_vec<RP>(tab + idx * Pitch<RP>::v, o);
     const float t = dot_fma<RP>(own, o);
-    float logP, g;
-    lik_grad<KIND, LOG>(t, pad ? 0 : code, edges, lk, logP, g);
+    float log2P, g;
+    lik_grad<KIND, LOG>(t, pad ? 0 : code, edges, lk, log2P, g);
     g = pad ? 0.0f : g;
-    nll -= pad ? 0.0f : logP;
+    nll -= pad ? 0.0f : log2P;  // in log2 units: scaled by ln 2 after the wave sum
 #pragma unroll
     for (int r = 0; r < RP; ++r) acc[r] = __builtin_fmaf(g, o[r], acc[r]);
 #if QSC_ENTRY_BARRIER
@@ -136,23 +136,46 @@ __device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const float 
   }
 }
 
-// Walk chunks j0, j0+js, j0+2js, ... < j1 of a lane list whose consecutive chunks are `row`
-// V4 units apart (two chunks in flight ahead of the one computed).
+// Read-ahead of a lane list in groups of NB chunks (chunk j at src[j * row], row in V4 units).
+// Loads are unconditional with the index clamped to the lane's last chunk (the entry arrays end
+// with a QSC_ENTRY_TAIL pad, so even an empty list's chunk 0 is addressable): the number of
+// loads in flight is static, so the compiler waits for exactly the group it consumes
+// (vmcnt(NB)) instead of draining every prefetch at a branch merge.
+constexpr int kGroup = 4;
+
+template <typename V4>
+__device__ __forceinline__ void load_group(const V4* __restrict__ src, int row, int jb, int js,
+                                           int jlast, V4 (&b)[kGroup]) {
+#pragma unroll
+  for (int i = 0; i < kGroup; ++i) {
+    const int j = min(jb + i * js, jlast);
+    b[i] = src[(int64_t)j * row];
+  }
+}
+
+// Consume group b (chunks jb, jb+js, ..., < j1), then walk the rest of the list with the next
+// group's loads issued ahead of the current group's arithmetic.
 template <int RP, typename E, int KIND, bool LOG>
-__device__ __forceinline__ void walk(const typename Ent<E>::V4* __restrict__ src, int row, int j0,
-                                     int j1, int js, const float (&own)[RP],
-                                     const float* __restrict__ tab,
-                                     const float2* __restrict__ edges, const Lik& lk,
-                                     float (&acc)[RP], float& nll) {
+__device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restrict__ src, int row,
+                                            int jb, int j1, int js,
+                                            typename Ent<E>::V4 (&b)[kGroup],
+                                            const float (&own)[RP], const float* __restrict__ tab,
+                                            const float2* __restrict__ edges, const Lik& lk,
+                                            float (&acc)[RP], float& nll) {
   using V4 = typename Ent<E>::V4;
-  V4 a = (j0 < j1) ? src[(int64_t)j0 * row] : V4{};
-  V4 b = (j0 + js < j1) ? src[(int64_t)(j0 + js) * row] : V4{};
-  for (int j = j0; j < j1; j += 2 * js) {
-    const V4 c0 = a, c1 = b;
-    if (j + 2 * js < j1) a = src[(int64_t)(j + 2 * js) * row];
-    if (j + 3 * js < j1) b = src[(int64_t)(j + 3 * js) * row];
-    chunk<RP, E, KIND, LOG>(c0, own, tab, edges, lk, acc, nll);
-    if (j + js < j1) chunk<RP, E, KIND, LOG>(c1, own, tab, edges, lk, acc, nll);
+  const int jlast = max(j1 - 1, 0);
+  for (;;) {
+    const int jn = jb + kGroup * js;
+    const bool more = jn < j1;
+    V4 nb[kGroup];
+    load_group(src, row, jn, js, jlast, nb);  // unconditional: static vmcnt accounting
+#pragma unroll
+    for (int i = 0; i < kGroup; ++i)
+      if (jb + i * js < j1) chunk<RP, E, KIND, LOG>(b[i], own, tab, edges, lk, acc, nll);
+    if (!more) break;
+#pragma unroll
+    for (int i = 0; i < kGroup; ++i) b[i] = nb[i];
+    jb = jn;
   }
 }
 
@@ -167,13 +190,46 @@ __global__ void __launch_bounds__(kSBlock, (Occ<RP, QSC_SPASS_WAVES>::v)) spass_
     float* __restrict__ vS, qsc_adam ad, float lambda_s, qsc_state* __restrict__ st,
     float* __restrict__ part_nll, float* __restrict__ part_nsq) {
   using T = Ent<E>;
+  using V4 = typename T::V4;
   constexpr int CP = Pitch<RP>::v;
+  constexpr int RH = RP / 2;  // rows updated per lane (parity split)
   // all LDS carved from the 16-B aligned dynamic region (no statics ahead of it)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   Scalars& sc = *reinterpret_cast<Scalars*>(smem);            // 32 B reserved
   float* Cl = smem + 8;                                        // [K][CP]
   float2* El = reinterpret_cast<float2*>(Cl + (size_t)K * CP);  // [nbins]
 
+  // a wave = one slice of QSC_SLICE (32) pixel positions, two lanes per pixel: lane half h
+  // walks the pixel's chunks h, h+2, ...; the halves' partial dS are summed by a lane swap and
+  // each half then updates the rows r with r % 2 == h
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int p = lane & (QSC_SLICE - 1), h = lane >> 5;
+  const int s = blockIdx.x * kSWaves + wave;
+  const bool live = s < nslices;  // wave-uniform
+  const int q = s * QSC_SLICE + p;
+
+  // 1. every global read of the wave is issued up front (one memory latency for all of them):
+  //    the first group of entry chunks, S[:, q] and (fused Adam) the moments of this lane's rows
+  V4 buf[kGroup];
+  float sv[RP], mv[RH], vv[RH];
+  int j1 = 0;
+  const V4* src = nullptr;
+  if (live) {
+    j1 = width[s] >> 2;
+    src = reinterpret_cast<const V4*>(ent + off[s]) + p;
+    load_group(src, QSC_SLICE, h, 2, max(j1 - 1, 0), buf);
+#pragma unroll
+    for (int r = 0; r < RP; ++r) sv[r] = S[(int64_t)min(r, R - 1) * Pp + q];
+    if (ADAM) {
+#pragma unroll
+      for (int i = 0; i < RH; ++i) {
+        const int64_t o = (int64_t)min(2 * i + h, R - 1) * Pp + q;
+        mv[i] = mS[o];
+        vv[i] = vS[o];
+      }
+    }
+  }
+  // 2. stage C^T (rows padded to CP) and the bin edges in LDS
   for (int i = threadIdx.x; i < K * RP; i += blockDim.x) {
     const int r = i / K, k = i - r * K;  // coalesced reads of C[r][k]
     Cl[k * CP + r] = (r < R) ? C[(int64_t)r * K + k] : 0.0f;
@@ -196,41 +252,36 @@ __global__ void __launch_bounds__(kSBlock, (Occ<RP, QSC_SPASS_WAVES>::v)) spass_
     }
   }
   __syncthreads();
-
-  // a wave = one slice of QSC_SLICE (32) pixel positions, two lanes per pixel: lane half h
-  // walks the pixel's chunks h, h+2, ...; the halves' partial dS are summed by a lane swap and
-  // each half then updates the rows r with r % 2 == h
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int p = lane & (QSC_SLICE - 1), h = lane >> 5;
-  const int s = blockIdx.x * kSWaves + wave;
-  if (s >= nslices) return;
-  const int q = s * QSC_SLICE + p;
-
-  float sv[RP], acc[RP];
+  if (!live) return;
 #pragma unroll
-  for (int r = 0; r < RP; ++r) {
-    sv[r] = (r < R) ? S[(int64_t)r * Pp + q] : 0.0f;
-    acc[r] = 0.0f;
-  }
+  for (int r = 0; r < RP; ++r) sv[r] = (r < R) ? sv[r] : 0.0f;
+
+  // 3. likelihood + gradient over the pixel's observed entries
+  float acc[RP];
+#pragma unroll
+  for (int r = 0; r < RP; ++r) acc[r] = 0.0f;
   float nll = 0.0f;
-  const typename T::V4* src = reinterpret_cast<const typename T::V4*>(ent + off[s]) + p;
-  walk<RP, E, KIND, LOG>(src, QSC_SLICE, h, width[s] >> 2, 2, sv, Cl, El, lk, acc, nll);
+  walk_groups<RP, E, KIND, LOG>(src, QSC_SLICE, h, j1, 2, buf, sv, Cl, El, lk, acc, nll);
 #pragma unroll
   for (int r = 0; r < RP; ++r) acc[r] += __shfl_xor(acc[r], 32, 64);
 
-  nll = wave_sum(nll);
+  nll = wave_sum(nll) * kLn2;
   if (ADAM) {
     float nsq = 0.0f;
 #pragma unroll
-    for (int r = 0; r < RP; ++r) {
-      if (r < R && (r & 1) == h) {
-        const int64_t i = (int64_t)r * Pp + q;
-        float pv = sv[r], m = mS[i], v = vS[i];
-        const float g = __fadd_rn(acc[r], __fmul_rn(pv, sc.coef));
+    for (int i = 0; i < RH; ++i) {
+      const int r = 2 * i + h;
+      // the lane's rows in register order: acc/sv index r = 2i + h (select, no dynamic index)
+      const float a = h ? acc[2 * i + 1] : acc[2 * i];
+      float pv = h ? sv[2 * i + 1] : sv[2 * i];
+      if (r < R) {
+        const int64_t o = (int64_t)r * Pp + q;
+        float m = mv[i], v = vv[i];
+        const float g = __fadd_rn(a, __fmul_rn(pv, sc.coef));
         adam_elem(pv, m, v, g, ad, sc.as);
-        S[i] = pv;
-        mS[i] = m;
-        vS[i] = v;
+        S[o] = pv;
+        mS[o] = m;
+        vS[o] = v;
         nsq = __builtin_fmaf(pv, pv, nsq);
       }
     }
@@ -238,8 +289,10 @@ __global__ void __launch_bounds__(kSBlock, (Occ<RP, QSC_SPASS_WAVES>::v)) spass_
     if (lane == 0) part_nsq[s] = nsq;
   } else {
 #pragma unroll
-    for (int r = 0; r < RP; ++r)
-      if (r < R && (r & 1) == h) dS[(int64_t)r * Pp + q] = acc[r];
+    for (int i = 0; i < RH; ++i) {
+      const int r = 2 * i + h;
+      if (r < R) dS[(int64_t)r * Pp + q] = h ? acc[2 * i + 1] : acc[2 * i];
+    }
   }
   if (lane == 0) part_nll[s] = nll;
 }
@@ -254,6 +307,7 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
     const float* __restrict__ S, const float* __restrict__ C, float* __restrict__ slab,
     float* __restrict__ part_nll) {
   using T = Ent<E>;
+  using V4 = typename T::V4;
   constexpr int SP = Pitch<RP>::v;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Sl = smem;                                              // [PT][SP]
@@ -263,11 +317,36 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   const int t = blockIdx.x;
   const int64_t q0 = (int64_t)t * PT;
   const int Kp = nks * 64;
-  // stage the pixel tile: one position per thread, R coalesced row reads, 16-B LDS writes
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int units = nks * split;
+
+  // 1. the wave's first unit: entry read-ahead and C[:, k] issued before the tile staging
+  int u = wave;
+  V4 buf[kGroup];
+  float cv[RP];
+  int j0 = 0, j1 = 0;
+  const V4* src = nullptr;
+  auto unit_begin = [&](int uu) {
+    const int ks = uu / split, part = uu - ks * split;
+    const int64_t wi = (int64_t)t * nks + ks;
+    const int W4 = width[wi] >> 2;
+    j0 = (W4 * part) / split;
+    j1 = (W4 * (part + 1)) / split;
+    src = reinterpret_cast<const V4*>(ent + off[wi]) + lane;
+    load_group(src, 64, j0, 1, max(j1 - 1, 0), buf);
+    const int k = min(ks * 64 + lane, K - 1);
+#pragma unroll
+    for (int r = 0; r < RP; ++r) cv[r] = C[(int64_t)min(r, R - 1) * K + k];
+  };
+  if (u < units) unit_begin(u);
+
+  // 2. stage the pixel tile: one position per thread, R coalesced row reads, 16-B LDS writes
   for (int ql = threadIdx.x; ql < PT; ql += blockDim.x) {
     float v[RP];
 #pragma unroll
-    for (int r = 0; r < RP; ++r) v[r] = (r < R) ? S[(int64_t)r * Pp + q0 + ql] : 0.0f;
+    for (int r = 0; r < RP; ++r) v[r] = S[(int64_t)min(r, R - 1) * Pp + q0 + ql];
+#pragma unroll
+    for (int r = 0; r < RP; ++r) v[r] = (r < R) ? v[r] : 0.0f;
 #pragma unroll
     for (int r = 0; r < RP; r += 4)
       *reinterpret_cast<float4*>(Sl + ql * SP + r) = make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
@@ -275,24 +354,18 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   for (int i = threadIdx.x; i < nbins; i += blockDim.x) El[i] = E_.e[i];
   __syncthreads();
 
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int units = nks * split;
-  for (int u = wave; u < units; u += kCWaves) {
+  for (; u < units; u += kCWaves) {
     const int ks = u / split, part = u - ks * split;
     const int k = ks * 64 + lane;
-    float cv[RP], acc[RP];
 #pragma unroll
-    for (int r = 0; r < RP; ++r) {
-      cv[r] = (r < R && k < K) ? C[(int64_t)r * K + k] : 0.0f;
-      acc[r] = 0.0f;
-    }
+    for (int r = 0; r < RP; ++r) cv[r] = (r < R && k < K) ? cv[r] : 0.0f;
+    float acc[RP];
+#pragma unroll
+    for (int r = 0; r < RP; ++r) acc[r] = 0.0f;
     float nll = 0.0f;
+    walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, cv, Sl, El, lk, acc, nll);
+    nll = wave_sum(nll) * kLn2;
     const int64_t wi = (int64_t)t * nks + ks;
-    const int W4 = width[wi] >> 2;
-    const int j0 = (W4 * part) / split, j1 = (W4 * (part + 1)) / split;
-    const typename T::V4* src = reinterpret_cast<const typename T::V4*>(ent + off[wi]) + lane;
-    walk<RP, E, KIND, LOG>(src, 64, j0, j1, 1, cv, Sl, El, lk, acc, nll);
-    nll = wave_sum(nll);
     if (split == 1) {
 #pragma unroll
       for (int r = 0; r < RP; ++r)
@@ -304,6 +377,7 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
         if (r < R) Pl[((size_t)part * R + r) * Kp + k] = acc[r];
       if (lane == 0) Nl[part * nks + ks] = nll;
     }
+    if (u + kCWaves < units) unit_begin(u + kCWaves);
   }
   if (split > 1) {
     __syncthreads();
@@ -517,7 +591,7 @@ __global__ void selftest_erf_kernel(const float* __restrict__ x, int n, float* _
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   out[i] = erff(x[i]);
-  out[n + i] = erf_bf(x[i]);
+  out[n + i] = erf_fast(x[i]);
 }
 
 // ---- workspace layout ----

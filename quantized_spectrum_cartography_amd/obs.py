@@ -96,8 +96,8 @@ class Observations:
                   _lib.ptr(self.c_off), _lib.ptr(ws), ws.numel(), desc, s)
         self.desc = desc
         et = torch.int32 if desc.wide else torch.int16
-        self.s_entries = torch.empty(max(desc.s_entries, 1), dtype=et, device=dev)
-        self.c_entries = torch.empty(max(desc.c_entries, 1), dtype=et, device=dev)
+        self.s_entries = torch.empty(desc.s_entries, dtype=et, device=dev)
+        self.c_entries = torch.empty(desc.c_entries, dtype=et, device=dev)
         _lib.call("qsc_obs_fill", _lib.ptr(codes), desc, _lib.ptr(perm), _lib.ptr(self.s_width),
                   _lib.ptr(self.s_off), _lib.ptr(self.c_width), _lib.ptr(self.c_off),
                   _lib.ptr(self.s_entries), _lib.ptr(self.c_entries), s)

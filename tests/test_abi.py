@@ -87,6 +87,7 @@ def test_host_constants_match_header():
     src = open(_lib.HEADER).read()
     defs = dict(re.findall(r"#define\s+(QSC_[A-Z0-9_]+)\s+(0x[0-9A-Fa-f]+|\d+)\b", src))
     assert int(defs["QSC_SLICE"]) == _lib.QSC_SLICE
+    assert int(defs["QSC_ENTRY_TAIL"]) == _lib.QSC_ENTRY_TAIL
     assert int(defs["QSC_MAX_R"]) == _lib.QSC_MAX_R
     assert int(defs["QSC_MAX_BOUNDS"]) == _lib.QSC_MAX_BOUNDS
     assert int(defs["QSC_EINVAL"]) == _lib.QSC_EINVAL
