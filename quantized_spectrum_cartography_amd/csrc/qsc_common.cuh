@@ -242,6 +242,88 @@ __device__ __forceinline__ void lik_grad(float t, int code, const float2* __rest
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Two-entry (packed) forms.  gfx950 issues a wave64 f32 VALU op every ~4 cycles whether it is
+// v_fma_f32 or v_pk_fma_f32 (measured, tools/micro/valu_rate.hip), so the polynomial / FMA
+// parts of the per-entry math are evaluated for two entries per instruction.
+// ------------------------------------------------------------------------------------
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2v splat2(float x) { return f2v{x, x}; }
+
+__device__ __forceinline__ f2v erf_fast2(f2v x) {
+  const f2v ax = __builtin_elementwise_abs(x);
+  f2v p = fma2(ax, splat2(bits(0x378e98abu)), splat2(bits(0xb9c68948u)));
+  p = fma2(ax, p, splat2(bits(0x3b7cd369u)));
+  p = fma2(ax, p, splat2(bits(0xbcc618b2u)));
+  p = fma2(ax, p, splat2(bits(0x3dda74e4u)));
+  p = fma2(ax, p, splat2(bits(0x3f228afdu)));
+  p = fma2(ax, p, splat2(bits(0x3e03c728u)));
+  p = fma2(ax, p, ax);
+  const f2v pe = p * splat2(bits(0xbfb8aa3bu));
+  const f2v big = splat2(1.0f) - f2v{__builtin_amdgcn_exp2f(pe.x), __builtin_amdgcn_exp2f(pe.y)};
+  const f2v t = x * x;
+  f2v q = fma2(splat2(bits(0xba1345e1u)), t, splat2(bits(0x3ba10414u)));
+  q = fma2(t, q, splat2(bits(0xbcdac9b8u)));
+  q = fma2(t, q, splat2(bits(0x3de703beu)));
+  q = fma2(t, q, splat2(bits(0xbec09330u)));
+  q = fma2(t, q, splat2(bits(0x3e0375d0u)));
+  const f2v small = fma2(ax, q, ax);
+  return f2v{__builtin_copysignf(ax.x < 1.0f ? small.x : big.x, x.x),
+             __builtin_copysignf(ax.y < 1.0f ? small.y : big.y, x.y)};
+}
+
+__device__ __forceinline__ f2v div_lik2(f2v x, const Lik& c) {
+  const f2v ia = splat2(c.inv_a);
+  const f2v q = x * ia;
+  const f2v r = fma2(-q, splat2(c.a), x);
+  return fma2(r, ia, q);
+}
+
+__device__ __forceinline__ f2v exp2_2(f2v x) {
+  return f2v{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+}
+__device__ __forceinline__ f2v rcp2(f2v x) {
+  return f2v{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)};
+}
+__device__ __forceinline__ f2v log2_2(f2v x) {
+  return f2v{__builtin_amdgcn_logf(x.x), __builtin_amdgcn_logf(x.y)};
+}
+
+// lik_grad for two entries (t.x with code c0, t.y with code c1)
+template <int KIND, bool LOG>
+__device__ __forceinline__ void lik_grad2(f2v t, int c0, int c1, const float2* __restrict__ edges,
+                                          const Lik& c, f2v& log2P, f2v& g) {
+  if (KIND == LIK_ONEBIT) {
+    const f2v z = div_lik2(splat2(c.thr) - t, c);
+    const f2v F = splat2(0.5f) * (splat2(1.0f) + erf_fast2(z));
+    const f2v Fc = splat2(1.0f) - F;
+    const bool z0 = (c0 == 0), z1 = (c1 == 0);
+    const f2v P = f2v{z0 ? F.x : Fc.x, z1 ? F.y : Fc.y};
+    const f2v e = exp2_2(z * z * splat2(kNegLog2e)) * splat2(c.kgrad);
+    const f2v rp = rcp2(P);
+    g = f2v{z0 ? e.x : -e.x, z1 ? e.y : -e.y} * rp;
+    log2P = log2_2(P);
+  } else {
+    f2v x = t, tinv = splat2(1.0f);
+    if (LOG) {
+      const f2v tp = t + splat2(c.offset);
+      x = f2v{logf(tp.x), logf(tp.y)};
+      tinv = rcp2(tp);
+    }
+    const float2 e0 = edges[c0], e1 = edges[c1];
+    const f2v u = div_lik2(f2v{e0.y, e1.y} - x, c);
+    const f2v w = div_lik2(f2v{e0.x, e1.x} - x, c);
+    const f2v P = splat2(0.5f) * (splat2(1.0f) + erf_fast2(u)) -
+                  splat2(0.5f) * (splat2(1.0f) + erf_fast2(w));
+    const f2v d = (exp2_2(u * u * splat2(kNegLog2e)) - exp2_2(w * w * splat2(kNegLog2e))) *
+                  splat2(c.kgrad);
+    g = d * rcp2(P) * tinv;
+    log2P = log2_2(P);
+  }
+}
+
 // One observed entry end to end: t is the linear reconstruction value; returns P and the
 // gradient of -log P w.r.t. t (chain rule through log(t + offset) in the log model).
 __device__ __forceinline__ void entry_grad(float t, int code, const float2* edges,
@@ -339,6 +421,30 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
   const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), s.bc2_sqrt), s.eps);
   p = __fadd_rn(p, __fdiv_rn(__fmul_rn(-s.step_size, m), denom));
   if (ad.project_nonneg && p < 0.0f) p = 0.0f;
+}
+
+// The same update with the S-side's 2M-element cost in mind: sqrt and the two divisions as a
+// hardware estimate plus one residual correction each (correctly rounded but for rare
+// near-halfway cases, i.e. within 1 ulp of the torch values), ~20 VALU instead of ~50.
+__device__ __forceinline__ float sqrt_fix(float v) {
+  const float s = __builtin_amdgcn_sqrtf(v);
+  const float e = __builtin_fmaf(-s, s, v);
+  const float h = 0.5f * __builtin_amdgcn_rcpf(s);
+  return v > 0.0f ? __builtin_fmaf(e, h, s) : s;
+}
+__device__ __forceinline__ float div_fix(float x, float y) {
+  const float ry = __builtin_amdgcn_rcpf(y);
+  const float q = x * ry;
+  const float r = __builtin_fmaf(-q, y, x);
+  return __builtin_fmaf(r, ry, q);
+}
+__device__ __forceinline__ void adam_elem_fast(float& p, float& m, float& v, float g,
+                                               const AdamScalars& s) {
+  m = __builtin_fmaf(s.w1, g - m, m);
+  const float vb = __fmul_rn(v, s.beta2);
+  v = __builtin_fmaf(__fmul_rn(s.w2, g), g, vb);
+  const float denom = __fadd_rn(div_fix(sqrt_fix(v), s.bc2_sqrt), s.eps);
+  p = __fadd_rn(p, div_fix(__fmul_rn(-s.step_size, m), denom));
 }
 
 }  // namespace qsc

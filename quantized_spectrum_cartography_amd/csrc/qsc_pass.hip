@@ -19,6 +19,8 @@
 //           (bitwise deterministic; no atomics).
 // The per-entry math (lik_grad, qsc_common.cuh) is branch-free so that the four entries of
 // a load chunk are independent instruction streams the scheduler can interleave.
+#include <algorithm>
+
 #include "qsc_common.cuh"
 
 using namespace qsc;
@@ -42,6 +44,12 @@ constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 template <int RP, int W>
 struct Occ {
   static constexpr int v = (RP > 8) ? (W > 4 ? 4 : W) : W;
+};
+// the persistent S-pass holds two slices' inputs in registers: ranks 8 and 16 get 256 VGPRs
+// (2 waves per SIMD, the resident grid of QSC_SPASS_BPC = 2)
+template <int RP, int EB, int W>
+struct OccS {
+  static constexpr int v = (RP >= 8) ? (W > 2 ? 2 : W) : W;
 };
 
 // LDS row pitch (floats) of an RP-float gathered row: 16-B aligned for ds_read_b128 and, for
@@ -80,24 +88,24 @@ struct Ent<uint32_t> {
   }
 };
 
+// LDS row of RP floats as RP/2 packed pairs (16-B reads)
 template <int RP>
-__device__ __forceinline__ float dot_fma(const float* s, const float* c) {
-  float t = s[0] * c[0];
-#pragma unroll
-  for (int r = 1; r < RP; ++r) t = __builtin_fmaf(s[r], c[r], t);
-  return t;
-}
-
-template <int RP>
-__device__ __forceinline__ void lds_vec(const float* base, float (&v)[RP]) {
+__device__ __forceinline__ void lds_row2(const float* base, f2v (&v)[RP / 2]) {
 #pragma unroll
   for (int r = 0; r < RP; r += 4) {
     const float4 x = *reinterpret_cast<const float4*>(base + r);
-    v[r] = x.x;
-    v[r + 1] = x.y;
-    v[r + 2] = x.z;
-    v[r + 3] = x.w;
+    v[r / 2] = f2v{x.x, x.y};
+    v[r / 2 + 1] = f2v{x.z, x.w};
   }
+}
+
+// t = sum_r own[r] * o[r], accumulated pairwise in r (RP/2 packed FMAs + one add)
+template <int RP>
+__device__ __forceinline__ float dot2(const f2v (&own)[RP / 2], const f2v (&o)[RP / 2]) {
+  f2v d = own[0] * o[0];
+#pragma unroll
+  for (int j = 1; j < RP / 2; ++j) d = fma2(own[j], o[j], d);
+  return d.x + d.y;
 }
 
 struct Scalars {
@@ -105,34 +113,47 @@ struct Scalars {
   AdamScalars as;
 };
 
-// Process one 4-entry chunk: `own` is the lane's register vector (S of the pixel or C of the
-// frequency bin), `tab` the LDS table of the other factor indexed by the entry's low bits.
+// Process one 4-entry chunk as two packed pairs: `own` is the lane's register vector (S of the
+// pixel or C of the frequency bin, r-pairs), `tab` the LDS table of the other factor indexed by
+// the entry's low bits.  Pad entries carry index 0 (a valid row) and code kPad; their gradient
+// and log-likelihood are masked.
 template <int RP, typename E, int KIND, bool LOG>
-__device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const float (&own)[RP],
+__device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const f2v (&own)[RP / 2],
                                       const float* __restrict__ tab,
                                       const float2* __restrict__ edges, const Lik& lk,
-                                      float (&acc)[RP], float& nll) {
+                                      f2v (&acc)[RP / 2], float& nll) {
   using T = Ent<E>;
   uint32_t e[4];
   T::unpack(v, e);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int code = (int)(e[u] >> T::kBits);
-    const bool pad = (code == T::kPad);
-    const int idx = pad ? 0 : (int)(e[u] & T::kMask);
-    float o[RP];
-    lds_vec<RP>(tab + idx * Pitch<RP>::v, o);
-    const float t = dot_fma<RP>(own, o);
-    float log2P, g;
-    lik_grad<KIND, LOG>(t, pad ? 0 : code, edges, lk, log2P, g);
-    g = pad ? 0.0f : g;
-    nll -= pad ? 0.0f : log2P;  // in log2 units: scaled by ln 2 after the wave sum
+  for (int u = 0; u < 4; u += 2) {
+    const int ca = (int)(e[u] >> T::kBits), cb = (int)(e[u + 1] >> T::kBits);
+    const bool pa = (ca == T::kPad), pb = (cb == T::kPad);
+    f2v oa[RP / 2], ob[RP / 2];
+#if QSC_DIAG_NOLDS  // diagnostic build: no gather (bounds the LDS share of the pass)
 #pragma unroll
-    for (int r = 0; r < RP; ++r) acc[r] = __builtin_fmaf(g, o[r], acc[r]);
-#if QSC_ENTRY_BARRIER
-    // one entry at a time: bounded register footprint (8 waves/SIMD) instead of intra-wave ILP
-    __builtin_amdgcn_sched_barrier(0);
+    for (int j = 0; j < RP / 2; ++j) {
+      oa[j] = own[j] + splat2((float)(e[u] & T::kMask));
+      ob[j] = own[j] + splat2((float)(e[u + 1] & T::kMask));
+    }
+#else
+    lds_row2<RP>(tab + (e[u] & T::kMask) * Pitch<RP>::v, oa);
+    lds_row2<RP>(tab + (e[u + 1] & T::kMask) * Pitch<RP>::v, ob);
 #endif
+    const f2v t = f2v{dot2<RP>(own, oa), dot2<RP>(own, ob)};
+    f2v log2P, g;
+#if QSC_DIAG_NOMATH  // diagnostic build: no likelihood arithmetic (bounds the VALU share)
+    g = t * splat2(1e-3f);
+    log2P = t;
+#else
+    lik_grad2<KIND, LOG>(t, pa ? 0 : ca, pb ? 0 : cb, edges, lk, log2P, g);
+#endif
+    const float ga = pa ? 0.0f : g.x, gb = pb ? 0.0f : g.y;
+    nll -= (pa ? 0.0f : log2P.x) + (pb ? 0.0f : log2P.y);  // log2 units: scaled by ln 2 later
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j) acc[j] = fma2(splat2(ga), oa[j], acc[j]);
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j) acc[j] = fma2(splat2(gb), ob[j], acc[j]);
   }
 }
 
@@ -159,9 +180,10 @@ template <int RP, typename E, int KIND, bool LOG>
 __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restrict__ src, int row,
                                             int jb, int j1, int js,
                                             typename Ent<E>::V4 (&b)[kGroup],
-                                            const float (&own)[RP], const float* __restrict__ tab,
+                                            const f2v (&own)[RP / 2],
+                                            const float* __restrict__ tab,
                                             const float2* __restrict__ edges, const Lik& lk,
-                                            float (&acc)[RP], float& nll) {
+                                            f2v (&acc)[RP / 2], float& nll) {
   using V4 = typename Ent<E>::V4;
   const int jlast = max(j1 - 1, 0);
   for (;;) {
@@ -182,15 +204,101 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
 // ---------------------------------------------------------------------------------------
 // S-pass
 // ---------------------------------------------------------------------------------------
+#if QSC_DIAG_STAMPS
+// diagnostic builds only: per-wave timestamps of the S-pass phases (s_memtime, shader clock)
+constexpr int kStampWaves = 4096, kStamps = 32;
+#endif
+constexpr int kStampLast = 31;
+#if QSC_DIAG_STAMPS
+__device__ unsigned long long g_stamps[kStampWaves * kStamps];
+#define STAMP(w, i)                                                                  \
+  do {                                                                               \
+    if ((threadIdx.x & 63) == 0 && (w) < kStampWaves && (i) < kStamps)               \
+      g_stamps[(w) * kStamps + (i)] = __builtin_amdgcn_s_memtime();                  \
+  } while (0)
+#else
+#define STAMP(w, i) \
+  do {              \
+  } while (0)
+#endif
+
+// x[l] + x[l ^ 32] in every lane (the same sum in both halves), through v_permlane32_swap
+__device__ __forceinline__ float half_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// a1 if odd else a0, as bit operations: a ternary on a lane-varying bit is turned into a
+// dynamically indexed register array (scratch) by the compiler
+__device__ __forceinline__ float pick(uint32_t oddmask, float a0, float a1) {
+  const uint32_t u0 = __float_as_uint(a0), u1 = __float_as_uint(a1);
+  return __uint_as_float(u0 ^ ((u0 ^ u1) & oddmask));
+}
+
+// Per-slice registers read from HBM: the first group of entry chunks, S[:, q] and (fused Adam)
+// the moments of the lane's rows.  Two sets live at once (current + prefetched next slice).
+template <int RP, typename E, bool ADAM>
+struct SliceIn {
+  typename Ent<E>::V4 buf[kGroup];
+  float sv[RP];
+  float mv[RP / 2], vv[RP / 2];
+  int j1;
+  const typename Ent<E>::V4* src;
+
+  __device__ __forceinline__ void assign(const SliceIn& o) {
+#pragma unroll
+    for (int i = 0; i < kGroup; ++i) buf[i] = o.buf[i];
+#pragma unroll
+    for (int r = 0; r < RP; ++r) sv[r] = o.sv[r];
+    if constexpr (ADAM) {
+#pragma unroll
+      for (int i = 0; i < RP / 2; ++i) {
+        mv[i] = o.mv[i];
+        vv[i] = o.vv[i];
+      }
+    }
+    j1 = o.j1;
+    src = o.src;
+  }
+};
+
+// Issue every global read of slice s for this lane (unconditional loads: static vmcnt).
+template <int RP, typename E, bool ADAM>
+__device__ __forceinline__ void slice_load(SliceIn<RP, E, ADAM>& in, const E* __restrict__ ent,
+                                           const int* __restrict__ width,
+                                           const int64_t* __restrict__ off, int s, int p, int h,
+                                           int R, int Pp, const float* __restrict__ S,
+                                           const float* __restrict__ mS,
+                                           const float* __restrict__ vS) {
+  using V4 = typename Ent<E>::V4;
+  in.j1 = width[s] >> 2;
+  in.src = reinterpret_cast<const V4*>(ent + off[s]) + p;
+  load_group(in.src, QSC_SLICE, h, 2, max(in.j1 - 1, 0), in.buf);
+  const int64_t q = (int64_t)s * QSC_SLICE + p;
+#pragma unroll
+  for (int r = 0; r < RP; ++r) in.sv[r] = S[(int64_t)min(r, R - 1) * Pp + q];
+  if constexpr (ADAM) {
+#pragma unroll
+    for (int i = 0; i < RP / 2; ++i) {
+      const int64_t o = (int64_t)min(2 * i + h, R - 1) * Pp + q;
+      in.mv[i] = mS[o];
+      in.vv[i] = vS[o];
+    }
+  }
+}
+
+// Persistent S-pass: a grid sized to the resident waves; wave w of W processes slices
+// w, 2W-1-w, 2W+w, ... (snake order over the count-sorted slices balances the work) and
+// reads slice i+1 while it computes slice i, so HBM traffic and arithmetic overlap for the
+// whole pass instead of alternating in lockstep across the grid.
 template <int RP, typename E, int KIND, bool LOG, bool ADAM>
-__global__ void __launch_bounds__(kSBlock, (Occ<RP, QSC_SPASS_WAVES>::v)) spass_kernel(
+__global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_WAVES>::v)) spass_kernel(
     const E* __restrict__ ent, const int* __restrict__ width, const int64_t* __restrict__ off,
     int nslices, Lik lk, Edges E_, int nbins, int R, int K, int Pp, float* __restrict__ S,
     const float* __restrict__ C, float* __restrict__ dS, float* __restrict__ mS,
     float* __restrict__ vS, qsc_adam ad, float lambda_s, qsc_state* __restrict__ st,
     float* __restrict__ part_nll, float* __restrict__ part_nsq) {
-  using T = Ent<E>;
-  using V4 = typename T::V4;
   constexpr int CP = Pitch<RP>::v;
   constexpr int RH = RP / 2;  // rows updated per lane (parity split)
   // all LDS carved from the 16-B aligned dynamic region (no statics ahead of it)
@@ -199,42 +307,44 @@ __global__ void __launch_bounds__(kSBlock, (Occ<RP, QSC_SPASS_WAVES>::v)) spass_
   float* Cl = smem + 8;                                        // [K][CP]
   float2* El = reinterpret_cast<float2*>(Cl + (size_t)K * CP);  // [nbins]
 
-  // a wave = one slice of QSC_SLICE (32) pixel positions, two lanes per pixel: lane half h
-  // walks the pixel's chunks h, h+2, ...; the halves' partial dS are summed by a lane swap and
-  // each half then updates the rows r with r % 2 == h
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // a wave = one slice of QSC_SLICE (32) pixel positions at a time, two lanes per pixel: lane
+  // half h walks the pixel's chunks h, h+2, ...; the halves' partial dS are summed by a lane
+  // swap and each half then updates the rows r with r % 2 == h
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   const int p = lane & (QSC_SLICE - 1), h = lane >> 5;
-  const int s = blockIdx.x * kSWaves + wave;
+  const uint32_t hmask = 0u - (uint32_t)h;
+  const int W = gridDim.x * kSWaves;
+  const int w = blockIdx.x * kSWaves + wave;
+  auto slice_of = [&](int i) { return i * W + ((i & 1) ? (W - 1 - w) : w); };
+  int i = 0, s = slice_of(0);
   const bool live = s < nslices;  // wave-uniform
-  const int q = s * QSC_SLICE + p;
+  STAMP(w, 0);
 
-  // 1. every global read of the wave is issued up front (one memory latency for all of them):
-  //    the first group of entry chunks, S[:, q] and (fused Adam) the moments of this lane's rows
-  V4 buf[kGroup];
-  float sv[RP], mv[RH], vv[RH];
-  int j1 = 0;
-  const V4* src = nullptr;
-  if (live) {
-    j1 = width[s] >> 2;
-    src = reinterpret_cast<const V4*>(ent + off[s]) + p;
-    load_group(src, QSC_SLICE, h, 2, max(j1 - 1, 0), buf);
+  // 1. C^T tile reads first (the LDS staging below waits only for them), then the first slice
+  const int k0 = threadIdx.x;
+  float c0[RP];
 #pragma unroll
-    for (int r = 0; r < RP; ++r) sv[r] = S[(int64_t)min(r, R - 1) * Pp + q];
-    if (ADAM) {
-#pragma unroll
-      for (int i = 0; i < RH; ++i) {
-        const int64_t o = (int64_t)min(2 * i + h, R - 1) * Pp + q;
-        mv[i] = mS[o];
-        vv[i] = vS[o];
-      }
-    }
-  }
+  for (int r = 0; r < RP; ++r) c0[r] = C[(int64_t)min(r, R - 1) * K + min(k0, K - 1)];
+  SliceIn<RP, E, ADAM> cur;
+  if (live) slice_load(cur, ent, width, off, s, p, h, R, Pp, S, mS, vS);
   // 2. stage C^T (rows padded to CP) and the bin edges in LDS
-  for (int i = threadIdx.x; i < K * RP; i += blockDim.x) {
-    const int r = i / K, k = i - r * K;  // coalesced reads of C[r][k]
-    Cl[k * CP + r] = (r < R) ? C[(int64_t)r * K + k] : 0.0f;
+  if (k0 < K) {
+#pragma unroll
+    for (int r = 0; r < RP; r += 4)
+      *reinterpret_cast<float4*>(Cl + k0 * CP + r) =
+          make_float4(r < R ? c0[r] : 0.0f, r + 1 < R ? c0[r + 1] : 0.0f,
+                      r + 2 < R ? c0[r + 2] : 0.0f, r + 3 < R ? c0[r + 3] : 0.0f);
   }
-  for (int i = threadIdx.x; i < nbins; i += blockDim.x) El[i] = E_.e[i];
+  for (int k = k0 + kSBlock; k < K; k += kSBlock) {
+    float v[RP];
+#pragma unroll
+    for (int r = 0; r < RP; ++r) v[r] = (r < R) ? C[(int64_t)r * K + k] : 0.0f;
+#pragma unroll
+    for (int r = 0; r < RP; r += 4)
+      *reinterpret_cast<float4*>(Cl + k * CP + r) = make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
+  }
+  for (int b = threadIdx.x; b < nbins; b += kSBlock) El[b] = E_.e[b];
   if (threadIdx.x == 0) {
     if (ADAM) {
       const float nrm = sqrtf(st->normsq_s);
@@ -252,49 +362,87 @@ __global__ void __launch_bounds__(kSBlock, (Occ<RP, QSC_SPASS_WAVES>::v)) spass_
     }
   }
   __syncthreads();
-  if (!live) return;
-#pragma unroll
-  for (int r = 0; r < RP; ++r) sv[r] = (r < R) ? sv[r] : 0.0f;
+  STAMP(w, 1);
 
-  // 3. likelihood + gradient over the pixel's observed entries
-  float acc[RP];
+  // NLL / ||S_new||^2 accumulate per lane over the wave's slices; one wave sum at the end goes
+  // to the wave's partial slot (fixed order for a given grid; the slots W..nslices-1 are zeroed)
+  float nll_acc = 0.0f, nsq_acc = 0.0f;
+  if (live) {
+    for (;;) {
+      const int sn = slice_of(i + 1);
+      const bool more = sn < nslices;  // wave-uniform
+      // 3. next slice's reads in flight during this slice's arithmetic (unconditional: a last
+      //    slice re-reads itself, cache-resident, so the wait counts stay static)
+      SliceIn<RP, E, ADAM> nxt;
+      slice_load(nxt, ent, width, off, more ? sn : s, p, h, R, Pp, S, mS, vS);
+      STAMP(w, 2 + 3 * i);
+      const int q = s * QSC_SLICE + p;
+      float sv[RP];
 #pragma unroll
-  for (int r = 0; r < RP; ++r) acc[r] = 0.0f;
-  float nll = 0.0f;
-  walk_groups<RP, E, KIND, LOG>(src, QSC_SLICE, h, j1, 2, buf, sv, Cl, El, lk, acc, nll);
+      for (int r = 0; r < RP; ++r) sv[r] = (r < R) ? cur.sv[r] : 0.0f;
+      f2v own[RP / 2];
 #pragma unroll
-  for (int r = 0; r < RP; ++r) acc[r] += __shfl_xor(acc[r], 32, 64);
+      for (int j = 0; j < RP / 2; ++j) own[j] = f2v{sv[2 * j], sv[2 * j + 1]};
 
-  nll = wave_sum(nll) * kLn2;
-  if (ADAM) {
-    float nsq = 0.0f;
+      // 4. likelihood + gradient over the pixel's observed entries
+      f2v accp[RP / 2];
 #pragma unroll
-    for (int i = 0; i < RH; ++i) {
-      const int r = 2 * i + h;
-      // the lane's rows in register order: acc/sv index r = 2i + h (select, no dynamic index)
-      const float a = h ? acc[2 * i + 1] : acc[2 * i];
-      float pv = h ? sv[2 * i + 1] : sv[2 * i];
-      if (r < R) {
-        const int64_t o = (int64_t)r * Pp + q;
-        float m = mv[i], v = vv[i];
-        const float g = __fadd_rn(a, __fmul_rn(pv, sc.coef));
-        adam_elem(pv, m, v, g, ad, sc.as);
-        S[o] = pv;
-        mS[o] = m;
-        vS[o] = v;
-        nsq = __builtin_fmaf(pv, pv, nsq);
+      for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
+      walk_groups<RP, E, KIND, LOG>(cur.src, QSC_SLICE, h, cur.j1, 2, cur.buf, own, Cl, El, lk,
+                                    accp, nll_acc);
+      STAMP(w, 3 + 3 * i);
+      // the two lane halves' partial dS: v_permlane32_swap (VALU) instead of an LDS shuffle
+      float acc[RP];
+#pragma unroll
+      for (int j = 0; j < RP / 2; ++j) {
+        acc[2 * j] = half_sum(accp[j].x);
+        acc[2 * j + 1] = half_sum(accp[j].y);
       }
-    }
-    nsq = wave_sum(nsq);
-    if (lane == 0) part_nsq[s] = nsq;
-  } else {
+
+      // 5. epilogue: fused Adam on the lane's rows, or the raw gradient
+      if constexpr (ADAM) {
 #pragma unroll
-    for (int i = 0; i < RH; ++i) {
-      const int r = 2 * i + h;
-      if (r < R) dS[(int64_t)r * Pp + q] = h ? acc[2 * i + 1] : acc[2 * i];
+        for (int j = 0; j < RH; ++j) {
+          const int r = 2 * j + h;
+          // the lane's rows in register order: index r = 2j + h (select, no dynamic index)
+          const float a = pick(hmask, acc[2 * j], acc[2 * j + 1]);
+          float pv = pick(hmask, sv[2 * j], sv[2 * j + 1]);
+          if (r < R) {
+            const int64_t o = (int64_t)r * Pp + q;
+            float m = cur.mv[j], v = cur.vv[j];
+            const float g = __fadd_rn(a, __fmul_rn(pv, sc.coef));
+            adam_elem_fast(pv, m, v, g, sc.as);
+            S[o] = pv;
+            mS[o] = m;
+            vS[o] = v;
+            nsq_acc = __builtin_fmaf(pv, pv, nsq_acc);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < RH; ++j) {
+          const int r = 2 * j + h;
+          if (r < R) dS[(int64_t)r * Pp + q] = pick(hmask, acc[2 * j], acc[2 * j + 1]);
+        }
+      }
+      STAMP(w, 4 + 3 * i);
+      if (!more) break;
+      cur.assign(nxt);
+      s = sn;
+      ++i;
     }
   }
-  if (lane == 0) part_nll[s] = nll;
+  STAMP(w, kStampLast);
+  const float nll_w = wave_sum(nll_acc) * kLn2;
+  if (lane == 0) part_nll[w] = nll_w;
+  if constexpr (ADAM) {
+    const float nsq_w = wave_sum(nsq_acc);
+    if (lane == 0) part_nsq[w] = nsq_w;
+  }
+  for (int z = W + w * 64 + lane; z < nslices; z += W * 64) {
+    part_nll[z] = 0.0f;
+    if constexpr (ADAM) part_nsq[z] = 0.0f;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -357,13 +505,22 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   for (; u < units; u += kCWaves) {
     const int ks = u / split, part = u - ks * split;
     const int k = ks * 64 + lane;
+    f2v own[RP / 2];
 #pragma unroll
-    for (int r = 0; r < RP; ++r) cv[r] = (r < R && k < K) ? cv[r] : 0.0f;
+    for (int j = 0; j < RP / 2; ++j)
+      own[j] = f2v{(2 * j < R && k < K) ? cv[2 * j] : 0.0f,
+                   (2 * j + 1 < R && k < K) ? cv[2 * j + 1] : 0.0f};
+    f2v accp[RP / 2];
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
+    float nll = 0.0f;
+    walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
     float acc[RP];
 #pragma unroll
-    for (int r = 0; r < RP; ++r) acc[r] = 0.0f;
-    float nll = 0.0f;
-    walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, cv, Sl, El, lk, acc, nll);
+    for (int j = 0; j < RP / 2; ++j) {
+      acc[2 * j] = accp[j].x;
+      acc[2 * j + 1] = accp[j].y;
+    }
     nll = wave_sum(nll) * kLn2;
     const int64_t wi = (int64_t)t * nks + ks;
     if (split == 1) {
@@ -544,7 +701,7 @@ __global__ void __launch_bounds__(kSBlock) supdate_kernel(
     const int64_t i = (int64_t)r * Pp + q;
     float p = S[i], m = mS[i], v = vS[i];
     const float g = __fadd_rn(gsrc[i], __fmul_rn(p, sc.coef));
-    adam_elem(p, m, v, g, ad, sc.as);
+    adam_elem_fast(p, m, v, g, sc.as);  // the fused S-pass's update (no projection on S)
     S[i] = p;
     mS[i] = m;
     vS[i] = v;
@@ -634,6 +791,25 @@ bool desc_ok(const qsc_obs_desc* d) {
 }
 
 int rp_of(int R) { return R <= 4 ? 4 : (R <= 8 ? 8 : 16); }
+
+// compute units of the current device (cached per device id)
+int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+      n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+// resident S-pass workgroups per CU (persistent grid); RP=16 needs twice the registers
+#ifndef QSC_SPASS_BPC
+#define QSC_SPASS_BPC 2
+#endif
 
 int split_of(int nks) {
   int s = 1;
@@ -733,7 +909,8 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
   const Lik lk = make_lik(m);
   const int kind = lik_kind(m);
   const int nslices = d->Pp / QSC_SLICE;
-  const dim3 grid((unsigned)ceil_div(nslices, kSWaves));
+  const int bpc = std::min(QSC_SPASS_BPC, RP >= 8 ? 2 : QSC_SPASS_WAVES);
+  const dim3 grid((unsigned)std::min<int64_t>(ceil_div(nslices, kSWaves), (int64_t)cu_count() * bpc));
   qsc_adam ad{};
   if (adam) ad = *adam;
   hipStream_t s = STREAM(stream);
@@ -832,6 +1009,13 @@ QSC_API int qsc_sumsq_small(const float* x, int32_t n, float* out, void* stream)
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }
+
+#if QSC_DIAG_STAMPS
+QSC_API int qsc_diag_stamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps),
+                                  sizeof(unsigned long long) * (size_t)std::min(n, kStampWaves * kStamps));
+}
+#endif
 
 QSC_API int qsc_selftest_erf(const float* x, int32_t n, float* out, void* stream) {
   if (n < 0 || !x || !out) return QSC_EINVAL;

@@ -43,15 +43,23 @@ def time_one(config, reps):
     e = sol.engine
 
     def tk(fn):
-        s = torch.cuda.current_stream()
-        fn()
-        torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(s)
-        for _ in range(reps):
+        # launches captured in a hipGraph and replayed: device time, not Python launch time
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
             fn()
-        b.record(s)
-        b.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(reps):
+                    fn()
+            g.replay()
+            s.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            g.replay()
+            b.record(s)
+            b.synchronize()
+        torch.cuda.current_stream().wait_stream(s)
         return a.elapsed_time(b) / reps * 1e3
 
     us_s = tk(lambda: e.spass(sol.S, sol.C, 1, mS=sol.mS, vS=sol.vS, adam=sol.adam_s,
