@@ -1,0 +1,197 @@
+"""CPU (gloo, world size 2): the K-slab sharding logic of distributed.KSlabSolver.
+
+The solver is written against a small engine interface (fused.PassEngine on the GPU).  Here it
+runs over a CPU emulation of that interface whose gradients come from the oracle's closed-form
+math (oracle/explicit.py, fp64), so the test checks the sharding itself: the per-slab C-passes,
+the all-reduced ||C||^2 of the non-squared regulariser, the all-reduce of the partial S-gradient
+and the replicated S update.  Two ranks, each holding half of the frequency bins, must reproduce
+a single-process run over all bins, and both must follow the reference op sequence
+(oracle/solver.py) within the parity tolerance.
+"""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import explicit
+from oracle import reference_ops as ro
+from oracle import solver as osolver
+
+from conftest import rel_fro
+
+R, I, J, K, ITERS = 3, 12, 10, 16, 6
+
+
+class _Obs:
+    """Observations stand-in: natural pixel order is the position order (Pp = P)."""
+
+    def __init__(self, Y, Wx):
+        self.K = Y.shape[0]
+        self.I, self.J = Y.shape[-2], Y.shape[-1]
+        self.P = self.Pp = self.I * self.J
+        self.Y = Y.reshape(self.K, -1).numpy()
+        self.Wx = Wx.reshape(self.K, -1).numpy()
+
+    def to_positions(self, X):
+        return X.detach().reshape(X.shape[0], self.P).to(torch.float32).clone()
+
+    def to_pixels(self, Xp):
+        return Xp.clone()
+
+
+class _CpuEngine:
+    """The PassEngine calls KSlabSolver makes, evaluated with the oracle's fp64 gradients and
+    torch.optim.Adam's update (state kept like the device qsc_state)."""
+
+    def __init__(self, obs, b, sigma):
+        self.obs, self.b, self.sigma = obs, b, sigma
+        self.hist_cap = 0
+        self.hist = torch.zeros(4)
+        self.st = dict(step_c=0, step_s=0, iter=0, normsq_s=0.0, nll_c=0.0, nll_s=0.0)
+
+    def _grad(self, S, C):
+        return explicit.nll_grad(S.double().numpy(), C.double().numpy(), self.obs.Y, self.obs.Wx,
+                                 self.b, self.sigma)
+
+    @staticmethod
+    def _adam(p, m, v, g, step, adam):
+        b1, b2 = adam.beta1, adam.beta2
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        denom = (v.sqrt() / math.sqrt(1 - b2 ** step)).add_(adam.eps)
+        p.addcdiv_(m, denom, value=-adam.lr / (1 - b1 ** step))
+        if adam.project_nonneg:
+            p.clamp_(min=0.0)
+
+    def init_state(self, S):
+        self.st["normsq_s"] = float((S.double() ** 2).sum())
+
+    def cpass(self, S, C):
+        nll, _, dC = self._grad(S, C)
+        self._dC, self.st["nll_c"] = torch.from_numpy(dC).float(), float(nll)
+
+    def sumsq(self, x, out):
+        out[0] = float((x.double() ** 2).sum())
+
+    def cfinish(self, C, mode, mC=None, vC=None, adam=None, lambda_c=0.0, normsq_ext=None, **kw):
+        nrm = math.sqrt(float(normsq_ext[0]))
+        g = self._dC + (lambda_c / nrm if nrm > 0 else 0.0) * C
+        self.st["step_c"] += 1
+        self._adam(C, mC, vC, g, self.st["step_c"], adam)
+
+    def spass(self, S, C, mode, dS=None, **kw):
+        nll, gS, _ = self._grad(S, C)
+        dS.copy_(torch.from_numpy(gS).float())
+        self.st["nll_s"] = float(nll)
+        self.st["iter"] += 1
+
+    def supdate(self, S, mS, vS, g, adam, lambda_s):
+        nrm = math.sqrt(self.st["normsq_s"])
+        gg = g + (lambda_s / nrm if nrm > 0 else 0.0) * S
+        self.st["step_s"] += 1
+        self._adam(S, mS, vS, gg, self.st["step_s"], adam)
+        self.st["normsq_s"] = float((S.double() ** 2).sum())
+
+    def flush(self, record=True):
+        pass
+
+    def read_state(self):
+        return dict(self.st)
+
+
+def _problem():
+    g = torch.Generator().manual_seed(11)
+    S_true = torch.rand(R, 1, I, J, generator=g)
+    C_true = torch.rand(R, K, generator=g)
+    T = ro.get_tensor(S_true, C_true)
+    thr = float(T.median())
+    sigma = (float(T.max()) - float(T.min())) / 4
+    b = torch.tensor([0.0, thr, float(T.max())])
+    Y = ro.quantize(T, sigma, b, noise=torch.randn(T.shape, generator=g)).unsqueeze(1)
+    Wx = torch.bernoulli(torch.full((K, 1, I, J), 0.4), generator=g)
+    S0 = 0.5 * torch.rand(R, 1, I, J, generator=g)
+    C0 = 0.5 * torch.rand(R, K, generator=g)
+    return S0, C0, Y, Wx, b, sigma
+
+
+class _SoloDist:
+    """torch.distributed stand-in for a one-process run (all-reduce = identity)."""
+
+    @staticmethod
+    def all_reduce(t, op=None):
+        return t
+
+    @staticmethod
+    def get_world_size():
+        return 1
+
+    @staticmethod
+    def all_gather(outs, t):
+        outs[0].copy_(t)
+
+
+def _run(dist_mod, rank, world):
+    from quantized_spectrum_cartography_amd.distributed import KSlabSolver, kslab_bounds
+    S0, C0, Y, Wx, b, sigma = _problem()
+    k0, k1 = kslab_bounds(K, world, rank)
+    obs = _Obs(Y[k0:k1], Wx[k0:k1])
+    eng = _CpuEngine(obs, b.numpy(), sigma)
+    sol = KSlabSolver(obs, S0, C0[:, k0:k1], dist=dist_mod, engine=eng)
+    sol.run(ITERS)
+    return sol.S_pixels().reshape(R, I * J), sol.C_global(), eng.read_state()
+
+
+def _worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        S, C, st = _run(dist, rank, world)
+        if rank == 0:
+            np.savez(out_path, S=S.numpy(), C=C.numpy(), step_s=st["step_s"])
+        else:
+            np.savez(out_path + ".r1", S=S.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_kslab_bounds_partition():
+    from quantized_spectrum_cartography_amd.distributed import kslab_bounds
+    for K_, W in [(16, 2), (17, 3), (256, 8), (5, 8)]:
+        spans = [kslab_bounds(K_, W, r) for r in range(W)]
+        assert spans[0][0] == 0 and spans[-1][1] == K_
+        assert all(a[1] == b_[0] for a, b_ in zip(spans, spans[1:]))
+        sizes = [e - s for s, e in spans]
+        assert max(sizes) - min(sizes) <= 1
+
+
+def test_kslab_two_ranks_match_single_process(tmp_path):
+    out = str(tmp_path / "r0.npz")
+    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True,
+                       start_method="spawn")
+    two = np.load(out)
+    r1 = np.load(out + ".r1.npz")
+    S1, C1, _ = _run(_SoloDist, 0, 1)
+    # S is replicated: both ranks hold the same (all-reduced gradient, same update)
+    assert np.array_equal(two["S"], r1["S"])
+    assert int(two["step_s"]) == ITERS
+    # sharded == single process up to the summation order of the partial S-gradients
+    assert rel_fro(two["S"], S1.numpy()) < 1e-6
+    assert rel_fro(two["C"], C1.numpy()) < 1e-6
+    # and both follow the reference op sequence
+    S0, C0, Y, Wx, b, sigma = _problem()
+    ref = osolver.free_s_solve(S0, C0, Y, Wx, b, sigma, n_iter=ITERS)
+    assert rel_fro(two["S"], ref["S"].reshape(R, -1).numpy()) < 1e-5
+    assert rel_fro(two["C"], ref["C"].numpy()) < 1e-5
