@@ -128,6 +128,8 @@ typedef struct qsc_obs_desc {
  * library / device
  * ------------------------------------------------------------------------------------- */
 QSC_API int qsc_version(void);
+/* rank padding of the position-order factor layout: 4, 8 or 16 (R <= QSC_MAX_R), else 0 */
+QSC_API int qsc_rank_pad(int32_t R);
 QSC_API const char* qsc_error_string(int code);
 /* synchronous: returns 0 if device `dev` is a gfx950 the code objects can run on */
 QSC_API int qsc_device_check(int dev);
@@ -212,7 +214,8 @@ QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t P
 QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* desc, const int32_t* perm,
                          const int32_t* s_width, const int64_t* s_off, const int32_t* c_width,
                          const int64_t* c_off, void* s_entries, void* c_entries, void* stream);
-/* gather/scatter between natural pixel order [R][P] and position order [R][Pp] */
+/* gather/scatter between natural pixel order [R][P] and position order [Pp][RP]
+ * (RP = qsc_rank_pad(R); rows R..RP-1 and positions of no pixel are zero-filled / ignored) */
 QSC_API int qsc_perm_gather(const float* nat, const int32_t* perm, int32_t R, int32_t P,
                             int32_t Pp, float* pos, void* stream);
 QSC_API int qsc_perm_scatter(const float* pos, const int32_t* perm, int32_t R, int32_t P,
@@ -226,10 +229,13 @@ QSC_API int qsc_perm_scatter(const float* pos, const int32_t* perm, int32_t R, i
  *   dS[r,p] = sum_k g C[r,k], dC[r,k] = sum_p g S[r,p]
  *   (replaces get_tensor -> log -> prob_probit -> -sum(Wx log P) -> autograd backward,
  *    qmc/qmc.ipynb :566-575 and :626-633)
- * S, mS, vS, dS are in position order [R][Pp]; C, mC, vC in [R][K].
+ * S, mS, vS, dS are in position order [Pp][RP] (pixel-major: a position's RP = qsc_rank_pad(R)
+ * values are one 16/32/64-byte row, rows r >= R zero); C, mC, vC in [R][K].
  * ------------------------------------------------------------------------------------- */
+/* Pass workspace: zero it once before its first use (the S-pass keeps a slice scheduler in it
+ * and leaves it zero on exit); one workspace serves one stream at a time. */
 QSC_API size_t qsc_pass_workspace_bytes(const qsc_obs_desc* d, int32_t R);
-/* zero the state; normsq_s = ||S||^2 of the initial S (S nullable: 0) */
+/* zero the state; normsq_s = ||S||^2 of the initial S ([Pp][RP] position order; nullable: 0) */
 QSC_API int qsc_state_init(qsc_state* st, const float* S, int32_t R, int32_t Pp, void* ws,
                            size_t ws_bytes, void* stream);
 /* S-pass.  mode 0: write dS (NLL gradient only, no regulariser) — used by the generator/DIP
@@ -257,7 +263,7 @@ QSC_API int qsc_cfinish(const qsc_obs_desc* d, int32_t R, float* C, int32_t mode
  * the end of a solve and between passes that are not followed by a qsc_cfinish. */
 QSC_API int qsc_state_flush(const qsc_obs_desc* d, int32_t R, qsc_state* st, float* hist,
                             int32_t hist_cap, void* ws, size_t ws_bytes, void* stream);
-/* S update from an externally reduced gradient g [R][Pp] (K-slab sharding, after the RCCL
+/* S update from an externally reduced gradient g [Pp][RP] (K-slab sharding, after the RCCL
  * all-reduce of the partial dS): g + lambda_s*S/||S||, Adam on S, ||S_new||^2 partials, with
  * the same state protocol as the fused qsc_spass mode 1. */
 QSC_API int qsc_supdate(const qsc_obs_desc* d, int32_t R, float* S, float* mS, float* vS,

@@ -345,24 +345,26 @@ __global__ void __launch_bounds__(kBlock) sumsq_finish_kernel(const double* __re
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) perm_gather_kernel(const float* __restrict__ nat,
                                                              const int* __restrict__ perm, int R,
-                                                             int P, int Pp,
+                                                             int RP, int P, int Pp,
                                                              float* __restrict__ pos) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= (int64_t)R * Pp) return;
-  const int64_t r = i / Pp, q = i - r * Pp;
+  if (i >= (int64_t)RP * Pp) return;
+  const int64_t q = i / RP;
+  const int r = (int)(i - q * RP);
   const int p = perm[q];
-  pos[i] = (p >= 0 && p < P) ? nat[r * P + p] : 0.0f;
+  pos[i] = (r < R && p >= 0 && p < P) ? nat[(int64_t)r * P + p] : 0.0f;
 }
 
 __global__ void __launch_bounds__(kBlock) perm_scatter_kernel(const float* __restrict__ pos,
                                                               const int* __restrict__ perm, int R,
-                                                              int P, int Pp,
+                                                              int RP, int P, int Pp,
                                                               float* __restrict__ nat) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= (int64_t)R * Pp) return;
-  const int64_t r = i / Pp, q = i - r * Pp;
+  if (i >= (int64_t)RP * Pp) return;
+  const int64_t q = i / RP;
+  const int r = (int)(i - q * RP);
   const int p = perm[q];
-  if (p >= 0 && p < P) nat[r * P + p] = pos[i];
+  if (r < R && p >= 0 && p < P) nat[(int64_t)r * P + p] = pos[i];
 }
 
 }  // namespace
@@ -381,7 +383,11 @@ __global__ void __launch_bounds__(kBlock) perm_scatter_kernel(const float* __res
 
 extern "C" {
 
-QSC_API int qsc_version(void) { return 1; }
+QSC_API int qsc_version(void) { return 2; }  // 2: position-order factors are [Pp][RP]
+
+QSC_API int qsc_rank_pad(int32_t R) {
+  return (R < 1 || R > QSC_MAX_R) ? 0 : (R <= 4 ? 4 : (R <= 8 ? 8 : 16));
+}
 
 QSC_API const char* qsc_error_string(int code) {
   if (code == QSC_OK) return "success";
@@ -564,20 +570,22 @@ QSC_API int qsc_sumsq(const float* x, int64_t n, float* out, void* ws, size_t ws
 
 QSC_API int qsc_perm_gather(const float* nat, const int32_t* perm, int32_t R, int32_t P,
                             int32_t Pp, float* pos, void* stream) {
-  if (R < 1 || P < 1 || Pp < P || !nat || !perm || !pos) return QSC_EINVAL;
-  const int64_t n = (int64_t)R * Pp;
+  const int RP = qsc_rank_pad(R);
+  if (RP == 0 || P < 1 || Pp < P || !nat || !perm || !pos) return QSC_EINVAL;
+  const int64_t n = (int64_t)RP * Pp;
   hipLaunchKernelGGL(perm_gather_kernel, dim3((unsigned)ceil_div(n, kBlock)), dim3(kBlock), 0,
-                     STREAM(stream), nat, perm, R, P, Pp, pos);
+                     STREAM(stream), nat, perm, R, RP, P, Pp, pos);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }
 
 QSC_API int qsc_perm_scatter(const float* pos, const int32_t* perm, int32_t R, int32_t P,
                              int32_t Pp, float* nat, void* stream) {
-  if (R < 1 || P < 1 || Pp < P || !nat || !perm || !pos) return QSC_EINVAL;
-  const int64_t n = (int64_t)R * Pp;
+  const int RP = qsc_rank_pad(R);
+  if (RP == 0 || P < 1 || Pp < P || !nat || !perm || !pos) return QSC_EINVAL;
+  const int64_t n = (int64_t)RP * Pp;
   hipLaunchKernelGGL(perm_scatter_kernel, dim3((unsigned)ceil_div(n, kBlock)), dim3(kBlock), 0,
-                     STREAM(stream), pos, perm, R, P, Pp, nat);
+                     STREAM(stream), pos, perm, R, RP, P, Pp, nat);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }

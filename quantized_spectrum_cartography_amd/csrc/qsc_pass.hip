@@ -8,17 +8,16 @@
 // with explicit gradients (include/qsc.h) over observed entries only.
 //
 // Work mapping (wave64):
-//   S-pass: one lane per pixel position; the lane walks its pixel's observed (k, code) list
-//           (S-format); S[:,p] and dS[:,p] stay in registers, C[:,k] is gathered from LDS.
-//           The Adam update of S is fused into the epilogue (no dS round trip through HBM).
-//   C-pass: one lane per frequency bin k of a pixel tile; the lane walks the tile's observed
-//           (pixel, code) list for its k (C-format); C[:,k] and dC[:,k] stay in registers,
-//           S[:,p] is gathered from an LDS copy of the tile.  With few k-slices the list of a
-//           slice is split over several waves (partials combined in LDS in a fixed order).
-//           Per-tile dC partials go to a slab that qsc_cfinish reduces in a fixed order
-//           (bitwise deterministic; no atomics).
-// The per-entry math (lik_grad, qsc_common.cuh) is branch-free so that the four entries of
-// a load chunk are independent instruction streams the scheduler can interleave.
+//   S-pass: persistent grid; a wave takes 32-pixel slices (two lanes per pixel, each walking
+//           half of the pixel's observed (k, code) list, S-format); S[p,:] and dS stay in
+//           registers, C[:,k] is gathered from an LDS copy of C^T; the Adam update of S is
+//           fused into the epilogue (no dS round trip through HBM).
+//   C-pass: a 4-wave workgroup per (pixel tile, 64-bin slice); lane = bin k walking a quarter
+//           of the tile's observed (pixel, code) list for k (C-format) against the tile's S rows
+//           in LDS; C[:,k] and dC[:,k] stay in registers.  Per-tile dC partials go to a slab
+//           that qsc_cfinish reduces in a fixed order (bitwise deterministic; no atomics).
+// The per-entry math (lik_grad2, qsc_common.cuh) is branch-free and evaluates two entries per
+// packed instruction where the math allows.
 #include <algorithm>
 
 #include "qsc_common.cuh"
@@ -29,8 +28,7 @@ namespace {
 
 constexpr int kSBlock = 256;   // S-pass / S-update: 4 waves = 4 slices of QSC_SLICE pixels
 constexpr int kSWaves = kSBlock / 64;
-constexpr int kCBlock = 1024;  // C-pass: 16 waves share one LDS pixel tile
-constexpr int kCWaves = kCBlock / 64;
+constexpr int kCBlock = 256;   // C-pass: 4 waves = 4 quarters of one (tile, 64-bin slice)
 constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 
 // occupancy targets (waves per SIMD) that bound the register allocation of the passes; the
@@ -163,6 +161,7 @@ __device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const f2v (&
 // loads in flight is static, so the compiler waits for exactly the group it consumes
 // (vmcnt(NB)) instead of draining every prefetch at a branch merge.
 constexpr int kGroup = 4;
+constexpr int kSchedQ = 16;  // S-pass slice queues (scheduler counters), QSC_PASS workspace
 
 template <typename V4>
 __device__ __forceinline__ void load_group(const V4* __restrict__ src, int row, int jb, int js,
@@ -208,7 +207,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
 // diagnostic builds only: per-wave timestamps of the S-pass phases (s_memtime, shader clock)
 constexpr int kStampWaves = 4096, kStamps = 32;
 #endif
-constexpr int kStampLast = 31;
+[[maybe_unused]] constexpr int kStampLast = 31;
 #if QSC_DIAG_STAMPS
 __device__ unsigned long long g_stamps[kStampWaves * kStamps];
 #define STAMP(w, i)                                                                  \
@@ -216,11 +215,42 @@ __device__ unsigned long long g_stamps[kStampWaves * kStamps];
     if ((threadIdx.x & 63) == 0 && (w) < kStampWaves && (i) < kStamps)               \
       g_stamps[(w) * kStamps + (i)] = __builtin_amdgcn_s_memtime();                  \
   } while (0)
+#define RSTAMP(w, i)                                                                 \
+  do {                                                                               \
+    if ((threadIdx.x & 63) == 0 && (w) < kStampWaves && (i) < kStamps)               \
+      g_stamps[(w) * kStamps + (i)] = __builtin_amdgcn_s_memrealtime();              \
+  } while (0)
 #else
 #define STAMP(w, i) \
   do {              \
   } while (0)
+#define RSTAMP(w, i) \
+  do {               \
+  } while (0)
 #endif
+
+// Sum over the 64 lanes in a fixed order without LDS traffic: xor-1/xor-2 quad permutes and
+// the row half-mirror / mirror DPP moves leave every lane of a 16-lane row holding the row sum;
+// the four row sums are read into scalars and added in row order.  Result uniform.
+__device__ __forceinline__ float dpp_f(float x, int ctrl) {
+  switch (ctrl) {  // the DPP control must be an immediate
+    case 0xB1: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));
+    case 0x4E: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, false));
+    case 0x141: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, false));
+    default: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xF, 0xF, false));
+  }
+}
+__device__ __forceinline__ float wave_sum_dpp(float x) {
+  x += dpp_f(x, 0xB1);   // quad_perm [1,0,3,2]
+  x += dpp_f(x, 0x4E);   // quad_perm [2,3,0,1]
+  x += dpp_f(x, 0x141);  // row_half_mirror
+  x += dpp_f(x, 0x140);  // row_mirror
+  const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
+  const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 16));
+  const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 32));
+  const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 48));
+  return ((a + b) + c) + d;
+}
 
 // x[l] + x[l ^ 32] in every lane (the same sum in both halves), through v_permlane32_swap
 __device__ __forceinline__ float half_sum(float x) {
@@ -234,6 +264,35 @@ __device__ __forceinline__ float half_sum(float x) {
 __device__ __forceinline__ float pick(uint32_t oddmask, float a0, float a1) {
   const uint32_t u0 = __float_as_uint(a0), u1 = __float_as_uint(a1);
   return __uint_as_float(u0 ^ ((u0 ^ u1) & oddmask));
+}
+
+// N consecutive floats (N = 2, 4, 8) of a position-order row: 8/16-byte vector accesses
+template <int N>
+__device__ __forceinline__ void ld_row(const float* __restrict__ src, float (&v)[N]) {
+  if constexpr (N == 2) {
+    const float2 x = *reinterpret_cast<const float2*>(src);
+    v[0] = x.x;
+    v[1] = x.y;
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; i += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(src + i);
+      v[i] = x.x;
+      v[i + 1] = x.y;
+      v[i + 2] = x.z;
+      v[i + 3] = x.w;
+    }
+  }
+}
+template <int N>
+__device__ __forceinline__ void st_row(float* __restrict__ dst, const float (&v)[N]) {
+  if constexpr (N == 2) {
+    *reinterpret_cast<float2*>(dst) = make_float2(v[0], v[1]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; i += 4)
+      *reinterpret_cast<float4*>(dst + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+  }
 }
 
 // Per-slice registers read from HBM: the first group of entry chunks, S[:, q] and (fused Adam)
@@ -264,43 +323,39 @@ struct SliceIn {
 };
 
 // Issue every global read of slice s for this lane (unconditional loads: static vmcnt).
+// Position-order rows are [Pp][RP]: the lane reads its pixel's whole S row and the half
+// [h*RP/2, (h+1)*RP/2) of the Adam moments it will update.
 template <int RP, typename E, bool ADAM>
 __device__ __forceinline__ void slice_load(SliceIn<RP, E, ADAM>& in, const E* __restrict__ ent,
                                            const int* __restrict__ width,
                                            const int64_t* __restrict__ off, int s, int p, int h,
-                                           int R, int Pp, const float* __restrict__ S,
+                                           const float* __restrict__ S,
                                            const float* __restrict__ mS,
                                            const float* __restrict__ vS) {
   using V4 = typename Ent<E>::V4;
   in.j1 = width[s] >> 2;
   in.src = reinterpret_cast<const V4*>(ent + off[s]) + p;
   load_group(in.src, QSC_SLICE, h, 2, max(in.j1 - 1, 0), in.buf);
-  const int64_t q = (int64_t)s * QSC_SLICE + p;
-#pragma unroll
-  for (int r = 0; r < RP; ++r) in.sv[r] = S[(int64_t)min(r, R - 1) * Pp + q];
+  const int64_t row = ((int64_t)s * QSC_SLICE + p) * RP;
+  ld_row<RP>(S + row, in.sv);
   if constexpr (ADAM) {
-#pragma unroll
-    for (int i = 0; i < RP / 2; ++i) {
-      const int64_t o = (int64_t)min(2 * i + h, R - 1) * Pp + q;
-      in.mv[i] = mS[o];
-      in.vv[i] = vS[o];
-    }
+    ld_row<RP / 2>(mS + row + h * (RP / 2), in.mv);
+    ld_row<RP / 2>(vS + row + h * (RP / 2), in.vv);
   }
 }
 
-// Persistent S-pass: a grid sized to the resident waves; wave w of W processes slices
-// w, 2W-1-w, 2W+w, ... (snake order over the count-sorted slices balances the work) and
-// reads slice i+1 while it computes slice i, so HBM traffic and arithmetic overlap for the
-// whole pass instead of alternating in lockstep across the grid.
+// Persistent S-pass: a grid sized to the resident waves; each wave reads slice i+1 while it
+// computes slice i, so HBM traffic and arithmetic overlap for the whole pass.  Per-slice NLL /
+// ||S_new||^2 partials (DPP wave sums) keep the reductions' order independent of the grid.
 template <int RP, typename E, int KIND, bool LOG, bool ADAM>
 __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_WAVES>::v)) spass_kernel(
     const E* __restrict__ ent, const int* __restrict__ width, const int64_t* __restrict__ off,
     int nslices, Lik lk, Edges E_, int nbins, int R, int K, int Pp, float* __restrict__ S,
     const float* __restrict__ C, float* __restrict__ dS, float* __restrict__ mS,
     float* __restrict__ vS, qsc_adam ad, float lambda_s, qsc_state* __restrict__ st,
-    float* __restrict__ part_nll, float* __restrict__ part_nsq) {
+    float* __restrict__ part_nll, float* __restrict__ part_nsq, int* __restrict__ sched) {
   constexpr int CP = Pitch<RP>::v;
-  constexpr int RH = RP / 2;  // rows updated per lane (parity split)
+  constexpr int RH = RP / 2;  // row elements updated per lane (half row)
   // all LDS carved from the 16-B aligned dynamic region (no statics ahead of it)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   Scalars& sc = *reinterpret_cast<Scalars*>(smem);            // 32 B reserved
@@ -309,25 +364,33 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
 
   // a wave = one slice of QSC_SLICE (32) pixel positions at a time, two lanes per pixel: lane
   // half h walks the pixel's chunks h, h+2, ...; the halves' partial dS are summed by a lane
-  // swap and each half then updates the rows r with r % 2 == h
+  // swap and each half then updates its half of the pixel's row
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int p = lane & (QSC_SLICE - 1), h = lane >> 5;
   const uint32_t hmask = 0u - (uint32_t)h;
   const int W = gridDim.x * kSWaves;
   const int w = blockIdx.x * kSWaves + wave;
-  auto slice_of = [&](int i) { return i * W + ((i & 1) ? (W - 1 - w) : w); };
-  int i = 0, s = slice_of(0);
-  const bool live = s < nslices;  // wave-uniform
+  // Static slice schedule: wave w of W takes slices w, 2W-1-w, 2W+w, 4W-1-w, ... (snake order
+  // over the count-sorted slices balances the per-wave work)
+  auto slice_of = [&](int t) { return t * W + ((t & 1) ? (W - 1 - w) : w); };
   STAMP(w, 0);
-
+  RSTAMP(w, 28);
+#if QSC_DIAG_STAMPS
+  if (lane == 0 && w < kStampWaves) {
+    g_stamps[w * kStamps + 26] = __builtin_amdgcn_s_getreg(0xF804);  // HW_ID: CU / SIMD / wave slot
+    g_stamps[w * kStamps + 27] = __builtin_amdgcn_s_getreg(0xF814);  // XCC_ID
+  }
+#endif
+  (void)sched;
+  int s = slice_of(0);
   // 1. C^T tile reads first (the LDS staging below waits only for them), then the first slice
   const int k0 = threadIdx.x;
   float c0[RP];
 #pragma unroll
   for (int r = 0; r < RP; ++r) c0[r] = C[(int64_t)min(r, R - 1) * K + min(k0, K - 1)];
   SliceIn<RP, E, ADAM> cur;
-  if (live) slice_load(cur, ent, width, off, s, p, h, R, Pp, S, mS, vS);
+  if (s < nslices) slice_load(cur, ent, width, off, s, p, h, S, mS, vS);
   // 2. stage C^T (rows padded to CP) and the bin edges in LDS
   if (k0 < K) {
 #pragma unroll
@@ -364,94 +427,94 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
   __syncthreads();
   STAMP(w, 1);
 
-  // NLL / ||S_new||^2 accumulate per lane over the wave's slices; one wave sum at the end goes
-  // to the wave's partial slot (fixed order for a given grid; the slots W..nslices-1 are zeroed)
-  float nll_acc = 0.0f, nsq_acc = 0.0f;
-  if (live) {
-    for (;;) {
-      const int sn = slice_of(i + 1);
-      const bool more = sn < nslices;  // wave-uniform
-      // 3. next slice's reads in flight during this slice's arithmetic (unconditional: a last
-      //    slice re-reads itself, cache-resident, so the wait counts stay static)
-      SliceIn<RP, E, ADAM> nxt;
-      slice_load(nxt, ent, width, off, more ? sn : s, p, h, R, Pp, S, mS, vS);
-      STAMP(w, 2 + 3 * i);
-      const int q = s * QSC_SLICE + p;
-      float sv[RP];
+  int i = 0;
+  while (s < nslices) {
+    const int s1 = slice_of(i + 1);
+    const bool more = s1 < nslices;  // wave-uniform
+    // 3. next slice's reads in flight during this slice's arithmetic (unconditional: a last
+    //    slice re-reads itself, cache-resident, so the wait counts stay static)
+    SliceIn<RP, E, ADAM> nxt;
+    slice_load(nxt, ent, width, off, more ? s1 : s, p, h, S, mS, vS);
+    STAMP(w, 2 + 3 * i);
+    const int64_t row = ((int64_t)s * QSC_SLICE + p) * RP;
+    float sv[RP];  // rows >= R are zero in HBM (position-order padding)
 #pragma unroll
-      for (int r = 0; r < RP; ++r) sv[r] = (r < R) ? cur.sv[r] : 0.0f;
-      f2v own[RP / 2];
+    for (int r = 0; r < RP; ++r) sv[r] = cur.sv[r];
+    f2v own[RP / 2];
 #pragma unroll
-      for (int j = 0; j < RP / 2; ++j) own[j] = f2v{sv[2 * j], sv[2 * j + 1]};
+    for (int j = 0; j < RP / 2; ++j) own[j] = f2v{sv[2 * j], sv[2 * j + 1]};
 
-      // 4. likelihood + gradient over the pixel's observed entries
-      f2v accp[RP / 2];
+    // 4. likelihood + gradient over the pixel's observed entries
+    f2v accp[RP / 2];
 #pragma unroll
-      for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
-      walk_groups<RP, E, KIND, LOG>(cur.src, QSC_SLICE, h, cur.j1, 2, cur.buf, own, Cl, El, lk,
-                                    accp, nll_acc);
-      STAMP(w, 3 + 3 * i);
-      // the two lane halves' partial dS: v_permlane32_swap (VALU) instead of an LDS shuffle
-      float acc[RP];
+    for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
+    float nll = 0.0f;
+    walk_groups<RP, E, KIND, LOG>(cur.src, QSC_SLICE, h, cur.j1, 2, cur.buf, own, Cl, El, lk,
+                                  accp, nll);
+    STAMP(w, 3 + 3 * i);
+    // the two lane halves' partial dS: v_permlane32_swap (VALU) instead of an LDS shuffle
+    float acc[RP];
 #pragma unroll
-      for (int j = 0; j < RP / 2; ++j) {
-        acc[2 * j] = half_sum(accp[j].x);
-        acc[2 * j + 1] = half_sum(accp[j].y);
-      }
-
-      // 5. epilogue: fused Adam on the lane's rows, or the raw gradient
-      if constexpr (ADAM) {
-#pragma unroll
-        for (int j = 0; j < RH; ++j) {
-          const int r = 2 * j + h;
-          // the lane's rows in register order: index r = 2j + h (select, no dynamic index)
-          const float a = pick(hmask, acc[2 * j], acc[2 * j + 1]);
-          float pv = pick(hmask, sv[2 * j], sv[2 * j + 1]);
-          if (r < R) {
-            const int64_t o = (int64_t)r * Pp + q;
-            float m = cur.mv[j], v = cur.vv[j];
-            const float g = __fadd_rn(a, __fmul_rn(pv, sc.coef));
-            adam_elem_fast(pv, m, v, g, sc.as);
-            S[o] = pv;
-            mS[o] = m;
-            vS[o] = v;
-            nsq_acc = __builtin_fmaf(pv, pv, nsq_acc);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < RH; ++j) {
-          const int r = 2 * j + h;
-          if (r < R) dS[(int64_t)r * Pp + q] = pick(hmask, acc[2 * j], acc[2 * j + 1]);
-        }
-      }
-      STAMP(w, 4 + 3 * i);
-      if (!more) break;
-      cur.assign(nxt);
-      s = sn;
-      ++i;
+    for (int j = 0; j < RP / 2; ++j) {
+      acc[2 * j] = half_sum(accp[j].x);
+      acc[2 * j + 1] = half_sum(accp[j].y);
     }
+
+    // 5. epilogue: fused Adam on the lane's half row, or the raw gradient.  Padding rows
+    //    (r >= R) have zero S, C and moments, so Adam keeps them exactly zero.
+    float a[RH], pv[RH];
+#pragma unroll
+    for (int j = 0; j < RH; ++j) {
+      a[j] = pick(hmask, acc[j], acc[RH + j]);
+      pv[j] = pick(hmask, sv[j], sv[RH + j]);
+    }
+    if constexpr (ADAM) {
+      float m[RH], v[RH], nsq = 0.0f;
+#pragma unroll
+      for (int j = 0; j < RH; ++j) {
+        m[j] = cur.mv[j];
+        v[j] = cur.vv[j];
+        const float g = __fadd_rn(a[j], __fmul_rn(pv[j], sc.coef));
+        adam_elem_fast(pv[j], m[j], v[j], g, sc.as);
+        nsq = __builtin_fmaf(pv[j], pv[j], nsq);
+      }
+      st_row<RH>(S + row + h * RH, pv);
+      st_row<RH>(mS + row + h * RH, m);
+      st_row<RH>(vS + row + h * RH, v);
+      nsq = wave_sum_dpp(nsq);
+      if (lane == 0) part_nsq[s] = nsq;
+    } else {
+      st_row<RH>(dS + row + h * RH, a);
+    }
+    nll = wave_sum_dpp(nll) * kLn2;
+    if (lane == 0) part_nll[s] = nll;
+    STAMP(w, 4 + 3 * i);
+    if (!more) break;
+    cur.assign(nxt);
+    s = s1;
+    ++i;
   }
   STAMP(w, kStampLast);
-  const float nll_w = wave_sum(nll_acc) * kLn2;
-  if (lane == 0) part_nll[w] = nll_w;
-  if constexpr (ADAM) {
-    const float nsq_w = wave_sum(nsq_acc);
-    if (lane == 0) part_nsq[w] = nsq_w;
-  }
-  for (int z = W + w * 64 + lane; z < nslices; z += W * 64) {
-    part_nll[z] = 0.0f;
-    if constexpr (ADAM) part_nsq[z] = 0.0f;
-  }
+  RSTAMP(w, 29);
 }
 
 // ---------------------------------------------------------------------------------------
 // C-pass
 // ---------------------------------------------------------------------------------------
+// One workgroup per (pixel tile, 64-bin frequency slice): 4 waves, each walking a quarter of
+// the slice's per-bin entry lists (lane = bin k) against the tile's S rows staged in LDS.
+// Small workgroups (several resident per CU, dispatched as others retire) let the hardware
+// balance the uneven lists and overlap one group's staging with another's arithmetic.  The
+// four quarters are summed in LDS in a fixed order and written as the tile's dC slab rows.
+// Block -> (tile, slice) map: the nks slices of a tile are given blocks that the round-robin
+// dispatcher places on one XCD (b, b+8, b+16, ...), so the tile's S rows are read from that
+// XCD's L2 after the first (speed only; any bijection is correct).
+constexpr int kCParts = kCBlock / 64;
+
 template <int RP, typename E, int KIND, bool LOG>
 __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_kernel(
     const E* __restrict__ ent, const int* __restrict__ width, const int64_t* __restrict__ off,
-    int nks, int split, int PT, Lik lk, Edges E_, int nbins, int R, int K, int Pp,
+    int nks, int PT, int xcd_map, Lik lk, Edges E_, int nbins, int R, int K,
     const float* __restrict__ S, const float* __restrict__ C, float* __restrict__ slab,
     float* __restrict__ part_nll) {
   using T = Ent<E>;
@@ -460,95 +523,89 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Sl = smem;                                              // [PT][SP]
   float2* El = reinterpret_cast<float2*>(Sl + (size_t)PT * SP);   // [nbins] (<= 254)
-  float* Pl = Sl + (size_t)PT * SP + 2 * 256;                     // split partials [split][R][Kp]
-  float* Nl = Pl + (split > 1 ? (size_t)split * R * nks * 64 : 0);  // [split][nks]
-  const int t = blockIdx.x;
+  float* Pl = Sl + (size_t)PT * SP + 2 * 256;                     // [kCParts][R][64]
+  float* Nl = Pl + (size_t)kCParts * R * 64;                      // [kCParts]
+  int t, ks;
+  if (xcd_map) {
+    const int j = blockIdx.x >> 3, x = blockIdx.x & 7;
+    t = (j / nks) * 8 + x;
+    ks = j - (j / nks) * nks;
+  } else {
+    t = blockIdx.x / nks;
+    ks = blockIdx.x - t * nks;
+  }
   const int64_t q0 = (int64_t)t * PT;
   const int Kp = nks * 64;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int units = nks * split;
+  const int part = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  [[maybe_unused]] const int wg = blockIdx.x * kCParts + part;  // (diagnostic stamps)
+  STAMP(wg, 0);
+  RSTAMP(wg, 28);
 
-  // 1. the wave's first unit: entry read-ahead and C[:, k] issued before the tile staging
-  int u = wave;
+  // 1. entry read-ahead of this wave's quarter of the lists and C[:, k], before the staging
+  const int64_t wi = (int64_t)t * nks + ks;
+  const int W4 = width[wi] >> 2;
+  const int j0 = (W4 * part) / kCParts, j1 = (W4 * (part + 1)) / kCParts;
+  const V4* src = reinterpret_cast<const V4*>(ent + off[wi]) + lane;
   V4 buf[kGroup];
+  load_group(src, 64, j0, 1, max(j1 - 1, 0), buf);
+  const int k = ks * 64 + lane;
   float cv[RP];
-  int j0 = 0, j1 = 0;
-  const V4* src = nullptr;
-  auto unit_begin = [&](int uu) {
-    const int ks = uu / split, part = uu - ks * split;
-    const int64_t wi = (int64_t)t * nks + ks;
-    const int W4 = width[wi] >> 2;
-    j0 = (W4 * part) / split;
-    j1 = (W4 * (part + 1)) / split;
-    src = reinterpret_cast<const V4*>(ent + off[wi]) + lane;
-    load_group(src, 64, j0, 1, max(j1 - 1, 0), buf);
-    const int k = min(ks * 64 + lane, K - 1);
 #pragma unroll
-    for (int r = 0; r < RP; ++r) cv[r] = C[(int64_t)min(r, R - 1) * K + k];
-  };
-  if (u < units) unit_begin(u);
+  for (int r = 0; r < RP; ++r) cv[r] = C[(int64_t)min(r, R - 1) * K + min(k, K - 1)];
 
-  // 2. stage the pixel tile: one position per thread, R coalesced row reads, 16-B LDS writes
-  for (int ql = threadIdx.x; ql < PT; ql += blockDim.x) {
-    float v[RP];
-#pragma unroll
-    for (int r = 0; r < RP; ++r) v[r] = S[(int64_t)min(r, R - 1) * Pp + q0 + ql];
-#pragma unroll
-    for (int r = 0; r < RP; ++r) v[r] = (r < R) ? v[r] : 0.0f;
-#pragma unroll
-    for (int r = 0; r < RP; r += 4)
-      *reinterpret_cast<float4*>(Sl + ql * SP + r) = make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
+  // 2. stage the pixel tile: its position rows are contiguous in [Pp][RP]; 16-B reads and
+  //    16-B LDS writes at the padded pitch SP
+  {
+    const float4* __restrict__ src4 = reinterpret_cast<const float4*>(S + q0 * RP);
+    constexpr int V = RP / 4;  // float4 per row
+#pragma unroll 4
+    for (int i = threadIdx.x; i < PT * V; i += kCBlock) {
+      const int ql = i / V, c = i - ql * V;
+      *reinterpret_cast<float4*>(Sl + ql * SP + 4 * c) = src4[i];
+    }
   }
-  for (int i = threadIdx.x; i < nbins; i += blockDim.x) El[i] = E_.e[i];
+  for (int i = threadIdx.x; i < nbins; i += kCBlock) El[i] = E_.e[i];
   __syncthreads();
+  STAMP(wg, 1);
 
-  for (; u < units; u += kCWaves) {
-    const int ks = u / split, part = u - ks * split;
-    const int k = ks * 64 + lane;
-    f2v own[RP / 2];
+  // 3. likelihood + gradient over the quarter lists
+  f2v own[RP / 2];
 #pragma unroll
-    for (int j = 0; j < RP / 2; ++j)
-      own[j] = f2v{(2 * j < R && k < K) ? cv[2 * j] : 0.0f,
-                   (2 * j + 1 < R && k < K) ? cv[2 * j + 1] : 0.0f};
-    f2v accp[RP / 2];
+  for (int j = 0; j < RP / 2; ++j)
+    own[j] = f2v{(2 * j < R && k < K) ? cv[2 * j] : 0.0f,
+                 (2 * j + 1 < R && k < K) ? cv[2 * j + 1] : 0.0f};
+  f2v accp[RP / 2];
 #pragma unroll
-    for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
-    float nll = 0.0f;
-    walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
-    float acc[RP];
+  for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
+  float nll = 0.0f;
+  walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+  STAMP(wg, 2);
+  nll = wave_sum_dpp(nll) * kLn2;
 #pragma unroll
-    for (int j = 0; j < RP / 2; ++j) {
-      acc[2 * j] = accp[j].x;
-      acc[2 * j + 1] = accp[j].y;
-    }
-    nll = wave_sum(nll) * kLn2;
-    const int64_t wi = (int64_t)t * nks + ks;
-    if (split == 1) {
-#pragma unroll
-      for (int r = 0; r < RP; ++r)
-        if (r < R) slab[((int64_t)t * R + r) * Kp + k] = acc[r];
-      if (lane == 0) part_nll[wi] = nll;
-    } else {
-#pragma unroll
-      for (int r = 0; r < RP; ++r)
-        if (r < R) Pl[((size_t)part * R + r) * Kp + k] = acc[r];
-      if (lane == 0) Nl[part * nks + ks] = nll;
-    }
-    if (u + kCWaves < units) unit_begin(u + kCWaves);
+  for (int j = 0; j < RP / 2; ++j) {
+    if (2 * j < R) Pl[((size_t)part * R + 2 * j) * 64 + lane] = accp[j].x;
+    if (2 * j + 1 < R) Pl[((size_t)part * R + 2 * j + 1) * 64 + lane] = accp[j].y;
   }
-  if (split > 1) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < R * Kp; i += blockDim.x) {
-      float a = Pl[i];
-      for (int p = 1; p < split; ++p) a += Pl[(size_t)p * R * Kp + i];
-      slab[(int64_t)t * R * Kp + i] = a;
-    }
-    for (int ks = threadIdx.x; ks < nks; ks += blockDim.x) {
-      float a = Nl[ks];
-      for (int p = 1; p < split; ++p) a += Nl[p * nks + ks];
-      part_nll[(int64_t)t * nks + ks] = a;
-    }
+  if (lane == 0) Nl[part] = nll;
+  __syncthreads();
+  STAMP(wg, 3);
+
+  // 4. fixed-order sum of the quarters -> slab rows of this tile / slice
+  for (int i = threadIdx.x; i < R * 64; i += kCBlock) {
+    float a = Pl[i];
+#pragma unroll
+    for (int pp = 1; pp < kCParts; ++pp) a += Pl[(size_t)pp * R * 64 + i];
+    const int r = i >> 6, l = i & 63;
+    slab[((int64_t)t * R + r) * Kp + ks * 64 + l] = a;
   }
+  if (threadIdx.x == 0) {
+    float a = Nl[0];
+#pragma unroll
+    for (int pp = 1; pp < kCParts; ++pp) a += Nl[pp];
+    part_nll[wi] = a;
+  }
+  STAMP(wg, kStampLast);
+  RSTAMP(wg, 29);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -678,11 +735,14 @@ __global__ void __launch_bounds__(1024) flush_kernel(qsc_state* __restrict__ st,
   }
 }
 
-// S update from an all-reduced gradient (K-slab): one thread per position, like the S-pass
+// S update from an all-reduced gradient (K-slab): the S-pass's lane mapping (32 positions per
+// wave, lane half h owns the row elements [h*RP/2, (h+1)*RP/2)) and its Adam
+template <int RP>
 __global__ void __launch_bounds__(kSBlock) supdate_kernel(
-    int nslices, int R, int Pp, float* __restrict__ S, float* __restrict__ mS,
-    float* __restrict__ vS, const float* __restrict__ gsrc, qsc_adam ad, float lambda_s,
-    qsc_state* __restrict__ st, float* __restrict__ part_nsq) {
+    int nslices, float* __restrict__ S, float* __restrict__ mS, float* __restrict__ vS,
+    const float* __restrict__ gsrc, qsc_adam ad, float lambda_s, qsc_state* __restrict__ st,
+    float* __restrict__ part_nsq) {
+  constexpr int RH = RP / 2;
   __shared__ Scalars sc;
   if (threadIdx.x == 0) {
     const float nrm = sqrtf(st->normsq_s);
@@ -691,22 +751,25 @@ __global__ void __launch_bounds__(kSBlock) supdate_kernel(
     if (blockIdx.x == 0) st->pending |= QSC_PEND_SUPD;  // normsq_s / step_s settled later
   }
   __syncthreads();
-  // same lane mapping as the S-pass: 32 positions per wave, rows split by parity
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int s = blockIdx.x * kSWaves + wave;
   if (s >= nslices) return;
-  const int q = s * QSC_SLICE + (lane & (QSC_SLICE - 1));
+  const int64_t o = ((int64_t)s * QSC_SLICE + (lane & (QSC_SLICE - 1))) * RP + (lane >> 5) * RH;
+  float p[RH], m[RH], v[RH], g[RH];
+  ld_row<RH>(S + o, p);
+  ld_row<RH>(mS + o, m);
+  ld_row<RH>(vS + o, v);
+  ld_row<RH>(gsrc + o, g);
   float nsq = 0.0f;
-  for (int r = lane >> 5; r < R; r += 2) {
-    const int64_t i = (int64_t)r * Pp + q;
-    float p = S[i], m = mS[i], v = vS[i];
-    const float g = __fadd_rn(gsrc[i], __fmul_rn(p, sc.coef));
-    adam_elem_fast(p, m, v, g, sc.as);  // the fused S-pass's update (no projection on S)
-    S[i] = p;
-    mS[i] = m;
-    vS[i] = v;
-    nsq = __builtin_fmaf(p, p, nsq);
+#pragma unroll
+  for (int j = 0; j < RH; ++j) {
+    const float gg = __fadd_rn(g[j], __fmul_rn(p[j], sc.coef));
+    adam_elem_fast(p[j], m[j], v[j], gg, sc.as);  // the fused S-pass's update (no projection)
+    nsq = __builtin_fmaf(p[j], p[j], nsq);
   }
+  st_row<RH>(S + o, p);
+  st_row<RH>(mS + o, m);
+  st_row<RH>(vS + o, v);
   nsq = wave_sum(nsq);
   if (lane == 0) part_nsq[s] = nsq;
 }
@@ -758,6 +821,7 @@ struct PassWs {
   float* snll;      // nslices
   float* snsq;      // nslices
   double* init;     // 256
+  int* sched;       // S-pass queue counters [kSchedQ] + finished-wave counter (zero between launches)
 };
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -775,13 +839,15 @@ PassWs carve(const qsc_obs_desc* d, int R, void* ws) {
   p.snsq = (float*)w;
   w += al((size_t)(d->Pp / QSC_SLICE) * 4);
   p.init = (double*)w;
+  w += al(256 * 8);
+  p.sched = (int*)w;
   return p;
 }
 
 size_t ws_bytes_for(const qsc_obs_desc* d, int R) {
   const int64_t Kp = (int64_t)d->nks * 64;
   return al((size_t)d->ntiles * R * Kp * 4) + al((size_t)d->ntiles * d->nks * 4) +
-         2 * al((size_t)(d->Pp / QSC_SLICE) * 4) + al(256 * 8);
+         2 * al((size_t)(d->Pp / QSC_SLICE) * 4) + al(256 * 8) + al((kSchedQ + 1) * 4);
 }
 
 bool desc_ok(const qsc_obs_desc* d) {
@@ -811,17 +877,10 @@ int cu_count() {
 #define QSC_SPASS_BPC 2
 #endif
 
-int split_of(int nks) {
-  int s = 1;
-  while (s * 2 * nks <= kCWaves) s *= 2;
-  return s;
-}
-
 size_t cpass_lds(const qsc_obs_desc* d, int R) {
-  const int RP = rp_of(R), split = split_of(d->nks);
-  size_t b = (size_t)d->PT * (RP == 4 ? 4 : RP + 4) * 4 + 2 * 256 * 4;
-  if (split > 1) b += (size_t)split * R * d->nks * 64 * 4 + (size_t)split * d->nks * 4;
-  return b;
+  const int RP = rp_of(R);
+  return (size_t)d->PT * (RP == 4 ? 4 : RP + 4) * 4 + 2 * 256 * 4 + (size_t)kCParts * R * 64 * 4 +
+         kCParts * 4;
 }
 
 }  // namespace
@@ -873,12 +932,13 @@ QSC_API size_t qsc_pass_workspace_bytes(const qsc_obs_desc* d, int32_t R) {
 
 QSC_API int qsc_state_init(qsc_state* st, const float* S, int32_t R, int32_t Pp, void* ws,
                            size_t ws_bytes, void* stream) {
-  if (!st || R < 1 || Pp < 1 || !ws || ws_bytes < 256 * sizeof(double)) return QSC_EINVAL;
+  if (!st || R < 1 || R > QSC_MAX_R || Pp < 1 || !ws || ws_bytes < 256 * sizeof(double))
+    return QSC_EINVAL;
   double* part = (double*)ws;
   const int nb = 256;
   if (S) {
     hipLaunchKernelGGL(nsq_part_kernel, dim3(nb), dim3(kSBlock), 0, STREAM(stream), S,
-                       (int64_t)R * Pp, part);
+                       (int64_t)rp_of(R) * Pp, part);  // [Pp][RP], padding rows are zero
     QSC_CHECK_LAUNCH();
   } else {
     QSC_TRY(hipMemsetAsync(part, 0, nb * sizeof(double), STREAM(stream)));
@@ -919,11 +979,13 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
     if (mode == 1)                                                                             \
       hipLaunchKernelGGL((spass_kernel<RPV, ET, KD, LG, true>), grid, dim3(kSBlock), shm, s,   \
                          (const ET*)s_entries, s_width, s_off, nslices, lk, E, d->nbins, R,    \
-                         d->K, d->Pp, S, C, dS, mS, vS, ad, lambda_s, st, w.snll, w.snsq);     \
+                         d->K, d->Pp, S, C, dS, mS, vS, ad, lambda_s, st, w.snll, w.snsq,       \
+                         w.sched);                                                             \
     else                                                                                       \
       hipLaunchKernelGGL((spass_kernel<RPV, ET, KD, LG, false>), grid, dim3(kSBlock), shm, s,  \
                          (const ET*)s_entries, s_width, s_off, nslices, lk, E, d->nbins, R,    \
-                         d->K, d->Pp, S, C, dS, mS, vS, ad, lambda_s, st, w.snll, w.snsq);     \
+                         d->K, d->Pp, S, C, dS, mS, vS, ad, lambda_s, st, w.snll, w.snsq,       \
+                         w.sched);                                                             \
   } while (0)
   QSC_DISPATCH_PASS(SPASS_LAUNCH);
 #undef SPASS_LAUNCH
@@ -941,17 +1003,18 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
   const int RP = rp_of(R);
   const size_t shm = cpass_lds(d, R);
   if (shm > 160 * 1024) return QSC_EINVAL;
-  const int split = split_of(d->nks);
   PassWs w = carve(d, R, ws);
   Edges E;
   make_edges(m, &E);
   const Lik lk = make_lik(m);
   const int kind = lik_kind(m);
   hipStream_t s = STREAM(stream);
+  const int xcd_map = (d->ntiles % 8) == 0 ? 1 : 0;
+  const dim3 grid((unsigned)((int64_t)d->ntiles * d->nks));
 #define CPASS_LAUNCH(RPV, ET, KD, LG)                                                          \
-  hipLaunchKernelGGL((cpass_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles), dim3(kCBlock), \
-                     shm, s, (const ET*)c_entries, c_width, c_off, d->nks, split, d->PT, lk, E, \
-                     d->nbins, R, d->K, d->Pp, S, C, w.slab, w.cnll)
+  hipLaunchKernelGGL((cpass_kernel<RPV, ET, KD, LG>), grid, dim3(kCBlock), shm, s,           \
+                     (const ET*)c_entries, c_width, c_off, d->nks, d->PT, xcd_map, lk, E,      \
+                     d->nbins, R, d->K, S, C, w.slab, w.cnll)
   QSC_DISPATCH_PASS(CPASS_LAUNCH);
 #undef CPASS_LAUNCH
   QSC_CHECK_LAUNCH();
@@ -997,8 +1060,15 @@ QSC_API int qsc_supdate(const qsc_obs_desc* d, int32_t R, float* S, float* mS, f
     return QSC_EINVAL;
   PassWs w = carve(d, R, ws);
   const int nslices = d->Pp / QSC_SLICE;
-  hipLaunchKernelGGL(supdate_kernel, dim3((unsigned)ceil_div(nslices, kSWaves)), dim3(kSBlock), 0,
-                     STREAM(stream), nslices, R, d->Pp, S, mS, vS, g, *adam, lambda_s, st, w.snsq);
+  const dim3 grid((unsigned)ceil_div(nslices, kSWaves)), blk(kSBlock);
+  const int RP = rp_of(R);
+  hipStream_t hs = STREAM(stream);
+  if (RP == 4)
+    hipLaunchKernelGGL(supdate_kernel<4>, grid, blk, 0, hs, nslices, S, mS, vS, g, *adam, lambda_s, st, w.snsq);
+  else if (RP == 8)
+    hipLaunchKernelGGL(supdate_kernel<8>, grid, blk, 0, hs, nslices, S, mS, vS, g, *adam, lambda_s, st, w.snsq);
+  else
+    hipLaunchKernelGGL(supdate_kernel<16>, grid, blk, 0, hs, nslices, S, mS, vS, g, *adam, lambda_s, st, w.snsq);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }

@@ -5,7 +5,7 @@ observations Y[k0:k1] and of the spectra C[:, k0:k1] — and a replica of S.  Pe
   C-step: local C-pass; the non-squared regulariser lambda_c ||C||_F needs the GLOBAL ||C||^2,
           so the ranks all-reduce one float before the fused cfinish (Adam + projection);
   S-step: local S-pass in gradient mode (partial dS over the slab's bins), an all-reduce of
-          dS (R x Pp fp32 — 8.4 MB at 512x512, R = 8), then the fused S update (regulariser,
+          dS (Pp x RP fp32 — 8.4 MB at 512x512, R = 8), then the fused S update (regulariser,
           Adam) on every rank; all ranks end with bit-identical S because the all-reduced dS is
           identical everywhere.
 The pixel order of S (positions) is derived from the GLOBAL per-pixel observation counts
@@ -92,7 +92,7 @@ class KSlabSolver:
         return self.engine.read_state()
 
     def S_pixels(self):
-        return self.obs.to_pixels(self.S).reshape(self.R, 1, self.obs.I, self.obs.J)
+        return self.obs.to_pixels(self.S, self.R).reshape(self.R, 1, self.obs.I, self.obs.J)
 
     def C_global(self):
         """All ranks' C slabs concatenated along K (collective)."""

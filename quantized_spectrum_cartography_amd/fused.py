@@ -27,7 +27,9 @@ class PassEngine:
         nb = _lib.lib().qsc_pass_workspace_bytes(obs.desc, R)
         if nb == 0:
             raise _lib.QscError("invalid observation descriptor")
-        self.ws = _ws(nb, dev)
+        # zeroed once: the S-pass keeps its slice scheduler words in the workspace and leaves
+        # them zero at exit (include/qsc.h, qsc_pass_workspace_bytes)
+        self.ws = torch.zeros(max(int(nb), 1), dtype=torch.uint8, device=dev)
         self.state = torch.zeros(_lib.STATE_BYTES, dtype=torch.uint8, device=dev)
         self.hist_cap = int(hist_cap)
         self.hist = torch.zeros(max(4 * self.hist_cap, 4), dtype=torch.float32, device=dev)
@@ -83,8 +85,7 @@ class PassEngine:
     # ---- composite ----------------------------------------------------------------------
     def nll_grad(self, S_pos, C, need_dS=True, need_dC=True):
         """NLL (device scalar) and its gradients dS (position order) and dC, no regularisers."""
-        R, Pp = self.R, self.obs.Pp
-        dS = torch.empty((R, Pp), dtype=torch.float32, device=S_pos.device) if need_dS else None
+        dS = torch.empty_like(S_pos) if need_dS else None
         dC = torch.empty_like(C) if need_dC else None
         if need_dC or not need_dS:
             self.cpass(S_pos, C)
@@ -106,7 +107,7 @@ class _ProbitNLLFn(torch.autograd.Function):
         Cd = _dev(C.detach().to(torch.float32)).contiguous()
         S_pos = obs.to_positions(S.detach().reshape(R, -1))
         nll, dS_pos, dC = eng.nll_grad(S_pos, Cd, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
-        dS = obs.to_pixels(dS_pos).reshape(S.shape) if dS_pos is not None else None
+        dS = obs.to_pixels(dS_pos, R).reshape(S.shape) if dS_pos is not None else None
         ctx.save_for_backward(*(t for t in (dS, dC) if t is not None))
         ctx.has = (dS is not None, dC is not None)
         return nll

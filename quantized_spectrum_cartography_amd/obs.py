@@ -13,14 +13,18 @@ from ._model import _dev, _ws
 
 
 def default_tile(P, R, K):
-    """C-pass pixel tile: ~512 tiles to fill 256 CUs, S tile in LDS <= 64 KB, <= 4096."""
+    """C-pass pixel tile (positions, a power of two in [128, 1024]).
+
+    The C-pass runs one 4-wave workgroup per (tile, 64-bin slice): aim for ~1024 workgroups
+    (4 per CU) while keeping tiles large, since the per-bin lists of a tile are padded to their
+    longest (bigger tiles -> relatively less padding) and the tile's S rows live in LDS."""
     Pp = -(-P // 64) * 64
-    rp = 4 if R <= 4 else (8 if R <= 8 else 16)
-    cap = min(4096, (64 * 1024) // (rp * 4))
-    cap -= cap % 64
-    want = max(64, -(-Pp // 512))
-    want = -(-want // 64) * 64
-    return min(want, cap)
+    nks = -(-K // 64)
+    want = max(1, (Pp * nks) // 1024)
+    t = 128
+    while t * 2 <= want and t < 1024:
+        t *= 2
+    return t
 
 
 class Observations:
@@ -119,20 +123,29 @@ class Observations:
                     c_padding=d.c_entries / max(d.nnz, 1) - 1.0)
 
     # ---- order conversions -------------------------------------------------------------
+    def rank_pad(self, R):
+        """Row count RP of the position-order layout for rank R (4, 8 or 16)."""
+        rp = int(_lib.lib().qsc_rank_pad(int(R)))
+        if rp == 0:
+            raise ValueError("rank R must be in [1, %d]" % _lib.QSC_MAX_R)
+        return rp
+
     def to_positions(self, X):
-        """(R, P) natural pixel order -> (R, Pp) position order."""
+        """(R, P) natural pixel order -> (Pp, RP) position order (pixel-major rows, zero padded)."""
         R = X.shape[0]
-        Xd = _dev(X.detach().to(torch.float32)).reshape(R, self.P)
-        out = torch.empty((R, self.Pp), dtype=torch.float32, device=Xd.device)
+        Xd = _dev(X.detach().to(torch.float32)).reshape(R, self.P).contiguous()
+        out = torch.empty((self.Pp, self.rank_pad(R)), dtype=torch.float32, device=Xd.device)
         _lib.call("qsc_perm_gather", _lib.ptr(Xd), _lib.ptr(self.perm), R, self.P, self.Pp,
                   _lib.ptr(out), _lib.stream())
         return out
 
-    def to_pixels(self, Xp, out=None):
-        """(R, Pp) position order -> (R, P) natural pixel order."""
-        R = Xp.shape[0]
+    def to_pixels(self, Xp, R, out=None):
+        """(Pp, RP) position order -> (R, P) natural pixel order."""
+        if Xp.shape != (self.Pp, self.rank_pad(R)):
+            raise ValueError("position-order tensor must be (%d, %d), got %s"
+                             % (self.Pp, self.rank_pad(R), tuple(Xp.shape)))
         if out is None:
             out = torch.empty((R, self.P), dtype=torch.float32, device=Xp.device)
-        _lib.call("qsc_perm_scatter", _lib.ptr(Xp), _lib.ptr(self.perm), R, self.P, self.Pp,
-                  _lib.ptr(out), _lib.stream())
+        _lib.call("qsc_perm_scatter", _lib.ptr(Xp.contiguous()), _lib.ptr(self.perm), R, self.P,
+                  self.Pp, _lib.ptr(out), _lib.stream())
         return out

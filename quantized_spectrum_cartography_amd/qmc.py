@@ -105,7 +105,7 @@ class FreeSSolver:
         return self.engine.read_state()
 
     def S_pixels(self):
-        return self.obs.to_pixels(self.S).reshape(self.R, 1, self.obs.I, self.obs.J)
+        return self.obs.to_pixels(self.S, self.R).reshape(self.R, 1, self.obs.I, self.obs.J)
 
     def history(self):
         self.engine.flush()  # settle the last S-pass (its history row)
@@ -231,7 +231,7 @@ def _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c
         S_pos = obs.to_positions(S.detach().reshape(R, -1))
         eng.spass(S_pos, C, 0, dS=dS_pos)
         eng.flush(record=False)
-        dS = obs.to_pixels(dS_pos).reshape(R, 1, I, J)
+        dS = obs.to_pixels(dS_pos, R).reshape(R, 1, I, J)
         reg = lambda_s * torch.norm(Z, "fro")
         surrogate = (S * dS).sum() + reg
         surrogate.backward()

@@ -40,7 +40,7 @@ class _Obs:
     def to_positions(self, X):
         return X.detach().reshape(X.shape[0], self.P).to(torch.float32).clone()
 
-    def to_pixels(self, Xp):
+    def to_pixels(self, Xp, R):
         return Xp.clone()
 
 

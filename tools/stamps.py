@@ -12,6 +12,34 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def cpass_timeline(sol, _lib, ctypes):
+    e = sol.engine
+    torch.cuda.synchronize()
+    e.cpass(sol.S, sol.C)
+    torch.cuda.synchronize()
+    L = _lib.lib()
+    n = 4096 * 32
+    buf = (ctypes.c_ulonglong * n)()
+    assert L.qsc_diag_stamps(buf, n) == 0
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 32).astype(np.int64)
+    st = st[st[:, 0] > 0]
+    r0 = st[:, 28].min()
+    pct = lambda x: "p10 %7.0f p50 %7.0f p90 %7.0f max %7.0f" % tuple(np.percentile(x, [10, 50, 90, 100]))
+    pct_us = lambda x: "p0 %6.2f p10 %6.2f p50 %6.2f p90 %6.2f max %6.2f us" % tuple(
+        np.percentile(x / 100.0, [0, 10, 50, 90, 100]))
+    print("C-pass: waves %d, span %.1f us" % (len(st), (st[:, 29].max() - r0) / 100.0))
+    print("  start", pct_us(st[:, 28] - r0))
+    print("  end  ", pct_us(st[:, 29] - r0))
+    print("  staging+barrier", pct(st[:, 1] - st[:, 0]))
+    ok = st[:, 2] > 0
+    print("  walk (waves with a unit)", pct(st[ok, 2] - st[ok, 1]))
+    print("  to LDS partials", pct(st[:, 3] - np.where(ok, st[:, 2], st[:, 1])))
+    ok4 = st[:, 4] > 0
+    if ok4.any():
+        print("  barrier wait", pct(st[ok4, 4] - st[ok4, 3]))
+        print("  reduce+slab", pct(st[ok4, 31] - st[ok4, 4]))
+
+
 def main():
     from quantized_spectrum_cartography_amd import _lib, synthetic
     from quantized_spectrum_cartography_amd.obs import Observations
@@ -41,6 +69,53 @@ def main():
     end = st[:, 31].max()
     print("kernel %.1f us (event); waves %d; span %d cycles -> %.2f GHz" % (
         us, len(st), end - t0, (end - t0) / (us * 1e3)))
+    rt = (st[:, 29] - st[:, 28]).astype(np.float64)  # s_memrealtime, 100 MHz
+    mt = (st[:, 31] - st[:, 0]).astype(np.float64)
+    print("shader clock from memtime/memrealtime: p50 %.2f GHz (wave lifetime p50 %.1f us)" % (
+        np.median(mt / rt) * 0.1, np.median(rt) / 100.0))
+    print("kernel span by memrealtime: %.1f us" % ((st[:, 29].max() - st[:, 28].min()) / 100.0))
+    r0 = st[:, 28].min()
+    pct_us = lambda x: "p0 %6.2f p10 %6.2f p50 %6.2f p90 %6.2f max %6.2f us" % tuple(
+        np.percentile(x / 100.0, [0, 10, 50, 90, 100]))
+    print("start (realtime)", pct_us(st[:, 28] - r0))
+    print("end   (realtime)", pct_us(st[:, 29] - r0))
+    # per-wave work (sum of its slices' widths) under the static snake schedule
+    W = 4096 if False else None
+    W = int(live.sum())
+    width = sol.obs.s_width.cpu().numpy().astype(np.int64)
+    ns = len(width)
+    work = np.zeros(W, np.int64)
+    for w in range(W):
+        t = 0
+        while True:
+            sidx = t * W + ((W - 1 - w) if (t & 1) else w)
+            if sidx >= ns:
+                break
+            work[w] += width[sidx]
+            t += 1
+    end_us = (st[:, 29] - r0) / 100.0
+    print("work per wave: min %d p50 %d max %d; corr(end, work) %.2f" % (
+        work.min(), np.median(work), work.max(), np.corrcoef(end_us, work)[0, 1]))
+    xcc = st[:, 27] & 0xF
+    for x in np.unique(xcc):
+        m = xcc == x
+        print("  xcc %d: waves %4d end p50 %.2f max %.2f us, work p50 %d" % (
+            x, m.sum(), np.median(end_us[m]), end_us[m].max(), np.median(work[m])))
+    hw = st[:, 26]
+    simd = (hw >> 4) & 3
+    cu = (hw >> 8) & 0xF
+    sh = (hw >> 12) & 1
+    se = (hw >> 13) & 7
+    key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+    pairs = {}
+    for idx in range(W):
+        pairs.setdefault((key[idx], simd[idx]), []).append(idx)
+    sw = np.array([work[v].sum() for v in pairs.values()])
+    se_end = np.array([end_us[v].max() for v in pairs.values()])
+    print("per-SIMD: waves/SIMD %s; work min %d p50 %d max %d; corr(SIMD end, SIMD work) %.2f" % (
+        np.bincount([len(v) for v in pairs.values()]), sw.min(), np.median(sw), sw.max(),
+        np.corrcoef(se_end, sw)[0, 1]))
+    cpass_timeline(sol, _lib, ctypes)
     rel = st - t0
     pct = lambda x: "p10 %7.0f p50 %7.0f p90 %7.0f max %7.0f" % tuple(np.percentile(x, [10, 50, 90, 100]))
     print("wave start     ", pct(rel[:, 0]))

@@ -28,14 +28,14 @@ def cmd_build(specs):
         print("built", name, fl, flush=True)
 
 
-def time_one(config, reps):
+def time_one(config, reps, tile=None):
     import torch
     from quantized_spectrum_cartography_amd import synthetic
     from quantized_spectrum_cartography_amd.obs import Observations
     from quantized_spectrum_cartography_amd.qmc import FreeSSolver
     I, J, K, R = synthetic.CONFIGS[config]
     prob = synthetic.onebit_problem(I, J, K, R, f=0.1, seed=20263, keep_T=False)
-    obs = Observations(prob["Y"], prob["Wx"], prob["b"], prob["sigma"], R_hint=R)
+    obs = Observations(prob["Y"], prob["Wx"], prob["b"], prob["sigma"], R_hint=R, tile=tile)
     sol = FreeSSolver(obs, prob["S0"], prob["C0"], hist_cap=64)
     sol.run(10)
     torch.cuda.synchronize()
@@ -68,7 +68,8 @@ def time_one(config, reps):
     us_f = tk(lambda: e.cfinish(sol.C, 1, mC=sol.mC, vC=sol.vC, adam=sol.adam_c,
                                 lambda_c=sol.lambda_c))
     return dict(spass_us=us_s, cpass_us=us_c, cfinish_us=us_f, nll_c=st["nll_c"],
-                nll_s=st["nll_s"], nnz=obs.nnz, tile=obs.desc.PT)
+                nll_s=st["nll_s"], nnz=obs.nnz, tile=obs.desc.PT,
+                c_pad=round(obs.stats()["c_padding"], 3), s_pad=round(obs.stats()["s_padding"], 3))
 
 
 def cmd_run(args):
@@ -79,9 +80,10 @@ def cmd_run(args):
         env = dict(os.environ)
         if name != "default":
             env["QSC_LIB_PATH"] = os.path.join(VDIR, "libqsc_%s.so" % name)
-        p = subprocess.run([sys.executable, __file__, "_one", "--config", args.config,
-                            "--reps", str(args.reps)], env=env, capture_output=True, text=True,
-                           timeout=300)
+        cmd = [sys.executable, __file__, "_one", "--config", args.config, "--reps", str(args.reps)]
+        if args.tile:
+            cmd += ["--tile", str(args.tile)]
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
         if p.returncode != 0:
             print(json.dumps({"variant": name, "rc": p.returncode, "err": p.stderr[-800:]}),
                   flush=True)
@@ -104,13 +106,14 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--names", default="")
     ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--tile", type=int, default=0)
     args = ap.parse_args()
     if args.mode == "build":
         cmd_build(args.specs)
     elif args.mode == "run":
         cmd_run(args)
     else:
-        print(json.dumps(time_one(args.config, args.reps)))
+        print(json.dumps(time_one(args.config, args.reps, args.tile or None)))
 
 
 if __name__ == "__main__":
