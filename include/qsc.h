@@ -251,14 +251,23 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
                       const int64_t* c_off, const qsc_model* m, int32_t R, const float* S,
                       const float* C, void* ws, size_t ws_bytes, void* stream);
 /* reduce the C-pass slab (fixed order).  mode 0: write dC (NLL gradient only); mode 1: fused
- * C-step: dC + lambda_c*C/||C||, Adam on C, projection.  Block 0 also records nll_c /
- * normsq_c and settles a pending S-pass (see qsc_state), appending history row
- * [nll_c, nll_s, normsq_c, normsq_s] of each completed iteration to hist (nullable).
+ * C-step: dC + lambda_c*C/||C||, Adam on C, projection; mode 2 (IJ-slab sharding): as mode 0 and
+ * dC[R*K] (dC holds R*K + 1 floats) receives this shard's ||S||^2 after the S-pass partials are
+ * settled, so one all-reduce carries both.  Block 0 also records nll_c / normsq_c and settles a
+ * pending S-pass (see qsc_state), appending history row [nll_c, nll_s, normsq_c, normsq_s] of
+ * each completed iteration to hist (nullable).
  * normsq_c_ext (device, nullable): global ||C||^2 supplied by the caller (K-slab sharding). */
 QSC_API int qsc_cfinish(const qsc_obs_desc* d, int32_t R, float* C, int32_t mode, float* dC,
                         float* mC, float* vC, const qsc_adam* adam, float lambda_c,
                         const float* normsq_c_ext, qsc_state* st, float* hist,
                         int32_t hist_cap, void* ws, size_t ws_bytes, void* stream);
+/* C update from an externally reduced gradient g [R][K] (IJ-slab sharding, after the RCCL
+ * all-reduce of the shards' dC): g + lambda_c*C/||C||, Adam on C, projection, with the state
+ * protocol of qsc_cfinish mode 1.  normsq_s_ext (device, nullable): the all-reduced ||S||^2,
+ * stored as the regulariser norm the next qsc_spass uses.  One workgroup (R*K is small). */
+QSC_API int qsc_cupdate(int32_t R, int32_t K, float* C, float* mC, float* vC, const float* g,
+                        const qsc_adam* adam, float lambda_c, const float* normsq_s_ext,
+                        qsc_state* st, void* stream);
 /* settle everything pending in st (S-pass partials, counters, history) — one block; used at
  * the end of a solve and between passes that are not followed by a qsc_cfinish. */
 QSC_API int qsc_state_flush(const qsc_obs_desc* d, int32_t R, qsc_state* st, float* hist,

@@ -704,7 +704,7 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
       mC[i] = m;
       vC[i] = v;
     } else {
-      dC[i] = g;
+      dC[i] = g;  // modes 0 and 2
     }
   }
   if (blockIdx.x == 0) {
@@ -718,7 +718,44 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
         st->normsq_c = nsq;
         st->pending |= QSC_PEND_C;
       }
+      if (mode == 2) dC[(int64_t)R * K] = st->normsq_s;  // this shard's ||S||^2 (IJ-slab)
     }
+  }
+}
+
+// C update from an externally reduced gradient g [R][K] (IJ-slab sharding, after the RCCL
+// all-reduce of the per-shard dC): g + lambda_c C/||C||, Adam, C >= 0; the same state
+// protocol as qsc_cfinish mode 1.  normsq_s_ext (nullable): the all-reduced ||S||^2, stored as
+// the S-pass's regulariser norm.
+__global__ void __launch_bounds__(kFBlock) cupdate_kernel(
+    int R, int K, float* __restrict__ C, float* __restrict__ mC, float* __restrict__ vC,
+    const float* __restrict__ g, qsc_adam ad, float lambda_c,
+    const float* __restrict__ normsq_s_ext, qsc_state* __restrict__ st) {
+  constexpr int NW = kFBlock / 64;
+  __shared__ float shn[NW];
+  __shared__ Scalars sc;
+  const int n = R * K;
+  float s2 = 0.0f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s2 = __builtin_fmaf(C[i], C[i], s2);
+  const float nsq = block_sum(s2, shn);
+  if (threadIdx.x == 0) {
+    const float nrm = sqrtf(nsq);
+    sc.coef = nrm > 0.0f ? lambda_c / nrm : 0.0f;
+    sc.as = adam_scalars(ad, st->step_c + 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    float p = C[i], m = mC[i], v = vC[i];
+    const float gg = __fadd_rn(g[i], __fmul_rn(p, sc.coef));
+    adam_elem(p, m, v, gg, ad, sc.as);
+    C[i] = p;
+    mC[i] = m;
+    vC[i] = v;
+  }
+  if (threadIdx.x == 0) {
+    st->normsq_c = nsq;
+    st->pending |= QSC_PEND_C;
+    if (normsq_s_ext) st->normsq_s = *normsq_s_ext;
   }
 }
 
@@ -1027,9 +1064,9 @@ QSC_API int qsc_cfinish(const qsc_obs_desc* d, int32_t R, float* C, int32_t mode
                         int32_t hist_cap, void* ws, size_t ws_bytes, void* stream) {
   if (!desc_ok(d) || R < 1 || R > QSC_MAX_R || !C || !st || !ws || ws_bytes < ws_bytes_for(d, R))
     return QSC_EINVAL;
-  if (mode == 0 && !dC) return QSC_EINVAL;
+  if ((mode == 0 || mode == 2) && !dC) return QSC_EINVAL;
   if (mode == 1 && (!mC || !vC || !adam)) return QSC_EINVAL;
-  if (mode != 0 && mode != 1) return QSC_EINVAL;
+  if (mode < 0 || mode > 2) return QSC_EINVAL;
   PassWs w = carve(d, R, ws);
   qsc_adam ad{};
   if (adam) ad = *adam;
@@ -1037,6 +1074,17 @@ QSC_API int qsc_cfinish(const qsc_obs_desc* d, int32_t R, float* C, int32_t mode
                      STREAM(stream), w.slab, d->ntiles, d->nks, R, d->K, C, mode, dC, mC, vC, ad,
                      lambda_c, normsq_c_ext, st, w.cnll, d->ntiles * d->nks, w.snll, w.snsq,
                      d->Pp / QSC_SLICE, hist, hist_cap);
+  QSC_CHECK_LAUNCH();
+  return QSC_OK;
+}
+
+QSC_API int qsc_cupdate(int32_t R, int32_t K, float* C, float* mC, float* vC, const float* g,
+                        const qsc_adam* adam, float lambda_c, const float* normsq_s_ext,
+                        qsc_state* st, void* stream) {
+  if (R < 1 || R > QSC_MAX_R || K < 1 || !C || !mC || !vC || !g || !adam || !st)
+    return QSC_EINVAL;
+  hipLaunchKernelGGL(cupdate_kernel, dim3(1), dim3(kFBlock), 0, STREAM(stream), R, K, C, mC, vC,
+                     g, *adam, lambda_c, normsq_s_ext, st);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }

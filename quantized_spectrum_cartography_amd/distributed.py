@@ -1,5 +1,15 @@
 """Multi-GPU sharding of the alternating solver over RCCL (torch.distributed, backend "nccl").
 
+Two layouts, both one process per GPU:
+
+IJ-slab (bench.py's default for N > 1): rank g owns a block of pixels — its observations
+Y[:, pixels] and its rows of S — and a replica of C (R x K, 8 KB at C3).  Per outer iteration
+  C-step: local C-pass and slab reduction (qsc_cfinish mode 2), one all-reduce of
+          [dC_local | ||S_local||^2] (R*K + 1 floats), the replicated C update (qsc_cupdate);
+  S-step: the fused local S-pass (likelihood, dS, Adam), whose lambda_s ||S||_F regulariser
+          uses the all-reduced ||S||^2 delivered by the C-step's collective.
+One small collective per iteration; S never crosses the fabric.
+
 K-slab (the north-star layout): rank g owns the frequency bins [k0, k1) — its slab of the
 observations Y[k0:k1] and of the spectra C[:, k0:k1] — and a replica of S.  Per outer iteration
   C-step: local C-pass; the non-squared regulariser lambda_c ||C||_F needs the GLOBAL ||C||^2,
@@ -41,6 +51,114 @@ def kslab_observations(Y_local, Wx_local, bin_boundaries, noise_std, dist, offse
                         log_model=log_model, tile=tile, R_hint=R_hint, count_hook=hook)
 
 
+def _capture(solver, iters):
+    """Capture `iters` iterations (kernels + RCCL collectives) in one hipGraph; None if the
+    backend refuses capture (the solver then runs eagerly)."""
+    try:
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(iters):
+                    solver.iteration()
+        torch.cuda.current_stream().wait_stream(s)
+        return g
+    except Exception:  # pragma: no cover - depends on the RCCL build
+        torch.cuda.synchronize()
+        return None
+
+
+def _run(solver, n, use_graph):
+    if use_graph and torch.cuda.is_available() and solver.S.is_cuda:
+        if solver._graph is None and not solver._graph_failed:
+            gi = 1 if n < 8 else 8
+            g = _capture(solver, gi)
+            if g is None:
+                solver._graph_failed = True
+            else:
+                solver._graph, solver._graph_iters = g, gi  # capture executes nothing
+        if solver._graph is not None:
+            k = n // solver._graph_iters
+            for _ in range(k):
+                solver._graph.replay()
+            n -= k * solver._graph_iters
+    for _ in range(n):
+        solver.iteration()
+
+
+class IJSlabSolver:
+    """Free-S alternating solver on one pixel block per rank (see module docstring)."""
+
+    def __init__(self, obs, S_init_local, C_init, dist, lambda_c=100.0, lambda_s=100.0,
+                 lr_c=5e-3, lr_s=1e-2, betas=(0.9, 0.999), eps=1e-8, project_c=True,
+                 hist_cap=1024, engine=None):
+        self.obs, self.dist = obs, dist
+        R = S_init_local.shape[0]
+        self.R = R
+        if engine is None:
+            from .fused import PassEngine
+            engine = PassEngine(obs, R, hist_cap=hist_cap)
+        self.engine = engine
+        self.S = obs.to_positions(S_init_local.reshape(R, -1))
+        dev = self.S.device
+        self.C = C_init.detach().to(dev, torch.float32).reshape(R, obs.K).clone()
+        self.mS, self.vS = torch.zeros_like(self.S), torch.zeros_like(self.S)
+        self.mC, self.vC = torch.zeros_like(self.C), torch.zeros_like(self.C)
+        # [dC_local (R*K) | ||S_local||^2]: the one all-reduced buffer of an iteration
+        self.red = torch.zeros(R * obs.K + 1, dtype=torch.float32, device=dev)
+        self.adam_c = _lib.make_adam(lr_c, betas, eps, project_nonneg=project_c)
+        self.adam_s = _lib.make_adam(lr_s, betas, eps, project_nonneg=False)
+        self.lambda_c, self.lambda_s = float(lambda_c), float(lambda_s)
+        self.engine.init_state(self.S)
+        self._graph, self._graph_iters, self._graph_failed = None, 0, False
+
+    def c_step(self):
+        e = self.engine
+        e.cpass(self.S, self.C)
+        e.cfinish(self.C, 2, dC=self.red)
+        self.dist.all_reduce(self.red)
+        e.cupdate(self.C, self.mC, self.vC, self.red, self.adam_c, self.lambda_c,
+                  normsq_s_ext=self.red[self.R * self.obs.K:])
+
+    def s_step(self):
+        self.engine.spass(self.S, self.C, 1, mS=self.mS, vS=self.vS, adam=self.adam_s,
+                          lambda_s=self.lambda_s)
+
+    def iteration(self):
+        self.c_step()
+        self.s_step()
+
+    def run(self, n, use_graph=False):
+        _run(self, n, use_graph)
+
+    def state(self):
+        return self.engine.read_state()
+
+    def S_pixels(self):
+        """This rank's pixel block of S, (R, 1, I_local, J)."""
+        return self.obs.to_pixels(self.S, self.R).reshape(self.R, 1, self.obs.I, self.obs.J)
+
+    def history(self):
+        """Global per-iteration costs (NLL columns summed over ranks; collective)."""
+        e = self.engine
+        e.flush()
+        st = e.read_state()
+        n = min(int(st["iter"]), e.hist_cap)
+        h = e.hist[: 4 * n].view(n, 4).clone()
+        nll = h[:, :2].contiguous()
+        self.dist.all_reduce(nll)
+        h = torch.cat([nll, h[:, 2:]], dim=1).double().cpu()
+        nsq_c_final = float((self.C.double() ** 2).sum().item())
+        costs_c, costs_s = [], []
+        for i in range(n):
+            nll_c, nll_s, nsq_c, nsq_s = h[i].tolist()
+            nsq_c_next = h[i + 1][2].item() if i + 1 < n else nsq_c_final
+            costs_c.append(nll_c + self.lambda_c * math.sqrt(nsq_c) + self.lambda_s * math.sqrt(nsq_s))
+            costs_s.append(nll_s + self.lambda_c * math.sqrt(nsq_c_next) + self.lambda_s * math.sqrt(nsq_s))
+        return costs_c, costs_s
+
+
 class KSlabSolver:
     """Free-S alternating solver on one K-slab per rank (see module docstring)."""
 
@@ -65,6 +183,7 @@ class KSlabSolver:
         self.adam_s = _lib.make_adam(lr_s, betas, eps, project_nonneg=False)
         self.lambda_c, self.lambda_s = float(lambda_c), float(lambda_s)
         self.engine.init_state(self.S)
+        self._graph, self._graph_iters, self._graph_failed = None, 0, False
 
     def c_step(self):
         e = self.engine
@@ -85,8 +204,7 @@ class KSlabSolver:
         self.s_step()
 
     def run(self, n, use_graph=False):
-        for _ in range(n):
-            self.iteration()
+        _run(self, n, use_graph)
 
     def state(self):
         return self.engine.read_state()

@@ -73,6 +73,12 @@ class PassEngine:
                   _lib.ptr(g), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),
                   self.ws.numel(), _lib.stream())
 
+    def cupdate(self, C, mC, vC, g, adam, lambda_c, normsq_s_ext=None):
+        """C update from an all-reduced gradient g (R*K [+1]) (IJ-slab sharding)."""
+        _lib.call("qsc_cupdate", self.R, self.obs.K, _lib.ptr(C), _lib.ptr(mC), _lib.ptr(vC),
+                  _lib.ptr(g), adam, float(lambda_c), _lib.ptr(normsq_s_ext),
+                  _lib.ptr(self.state), _lib.stream())
+
     def sumsq(self, x, out):
         """out[0] = ||x||^2 (fixed order, one workgroup; for small vectors such as C)."""
         _lib.call("qsc_sumsq_small", _lib.ptr(x), x.numel(), _lib.ptr(out), _lib.stream())

@@ -213,7 +213,7 @@ def _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c
                 cand = torch.randn((R, Z.shape[1]), dtype=torch.float32)
                 with torch.no_grad():
                     out = generator(cand.to(dev)).reshape(R, 1, I, J)
-                crit = nll_of(out) + lambda_c * float(torch.norm(C)) + lambda_s * float(torch.norm(S))
+                crit = nll_of(out) + lambda_c * float(torch.norm(C)) + lambda_s * float(torch.norm(S.detach()))
                 last = out
                 if crit < best:
                     Z.data = cand.to(dev).clone()
@@ -221,7 +221,7 @@ def _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c
             for _ in range(n2):
                 # the reference re-evaluates the last first-round sample here (temp_out, :611)
                 cand = 0.2 * torch.randn((R, Z.shape[1]), dtype=torch.float32) + Z.detach().cpu()
-                crit = nll_of(last) + lambda_c * float(torch.norm(C)) + lambda_s * float(torch.norm(S))
+                crit = nll_of(last) + lambda_c * float(torch.norm(C)) + lambda_s * float(torch.norm(S.detach()))
                 if crit < best:
                     Z.data = cand.to(dev).clone()
                     best = crit

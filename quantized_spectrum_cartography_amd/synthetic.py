@@ -73,6 +73,39 @@ def kslab_onebit_problem(I, J, K_local, R, rank, world, dist=None, f=0.1, seed=2
                 log_model=False, offset=0.0, thr=thr, T_true=T)
 
 
+def ijslab_onebit_problem(I, J, K, R, rank, world, dist=None, f=0.1, seed=20260,
+                          device="cuda"):
+    """One rank's pixel block of a global one-bit problem on an (I * world) x J grid.
+
+    C_true and C0 are common to all ranks (same seed); S_true / S0, the noise and the mask are
+    drawn per block.  The quantizer (thr = mean of the blocks' medians, sigma from the global
+    min/max) is agreed over `dist` so that all blocks share one probit model."""
+    g = torch.Generator().manual_seed(seed)
+    C_true = torch.rand(R, K, generator=g)
+    C0 = 0.5 * torch.rand(R, K, generator=g)
+    gl = torch.Generator().manual_seed(seed + 2000 + rank)
+    S_true = torch.rand(R, 1, I, J, generator=gl)
+    S0 = 0.5 * torch.rand(R, 1, I, J, generator=gl)
+    T = _model.get_tensor(S_true.to(device), C_true.to(device))
+    stats = torch.tensor([float(T.median()), -float(T.min()), float(T.max())], dtype=torch.float64,
+                         device=device)
+    if dist is not None and world > 1:
+        med = stats[:1].clone()
+        dist.all_reduce(med)
+        mx = stats[1:].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        stats = torch.cat([med / world, mx])
+    thr, tmin, tmax = float(stats[0]), -float(stats[1]), float(stats[2])
+    sigma = (tmax - tmin) / 4
+    b = torch.tensor([0.0, thr, tmax])
+    noise = torch.randn(T.shape, generator=gl)
+    Y = _model.quantize(T, sigma, b, noise=noise).unsqueeze(1)
+    del noise
+    Wx = torch.bernoulli(torch.full((K, 1, I, J), f), generator=gl)
+    return dict(S_true=S_true, C_true=C_true, b=b, sigma=sigma, Y=Y, Wx=Wx, S0=S0, C0=C0,
+                log_model=False, offset=0.0, thr=thr, T_true=T)
+
+
 CONFIGS = {
     # name: (I, J, K, R)   BASELINE.json configs
     "c2": (256, 256, 64, 4),

@@ -1,4 +1,4 @@
-"""CPU (gloo, world size 2): the K-slab sharding logic of distributed.KSlabSolver.
+"""CPU (gloo, world size 2): the sharding logic of distributed.KSlabSolver and IJSlabSolver.
 
 The solver is written against a small engine interface (fused.PassEngine on the GPU).  Here it
 runs over a CPU emulation of that interface whose gradients come from the oracle's closed-form
@@ -78,17 +78,39 @@ class _CpuEngine:
     def sumsq(self, x, out):
         out[0] = float((x.double() ** 2).sum())
 
-    def cfinish(self, C, mode, mC=None, vC=None, adam=None, lambda_c=0.0, normsq_ext=None, **kw):
+    def cfinish(self, C, mode, dC=None, mC=None, vC=None, adam=None, lambda_c=0.0,
+                normsq_ext=None, **kw):
+        if mode == 2:  # IJ-slab: local gradient + this shard's ||S||^2
+            n = C.numel()
+            dC[:n] = self._dC.reshape(-1)
+            dC[n] = self.st["normsq_s"]
+            return
         nrm = math.sqrt(float(normsq_ext[0]))
         g = self._dC + (lambda_c / nrm if nrm > 0 else 0.0) * C
         self.st["step_c"] += 1
         self._adam(C, mC, vC, g, self.st["step_c"], adam)
 
-    def spass(self, S, C, mode, dS=None, **kw):
+    def cupdate(self, C, mC, vC, g, adam, lambda_c, normsq_s_ext=None):
+        nrm = math.sqrt(float((C.double() ** 2).sum()))
+        gg = g[:C.numel()].reshape(C.shape) + (lambda_c / nrm if nrm > 0 else 0.0) * C
+        self.st["step_c"] += 1
+        self._adam(C, mC, vC, gg, self.st["step_c"], adam)
+        if normsq_s_ext is not None:
+            self.st["normsq_s"] = float(normsq_s_ext[0])
+
+    def spass(self, S, C, mode, dS=None, mS=None, vS=None, adam=None, lambda_s=0.0):
         nll, gS, _ = self._grad(S, C)
-        dS.copy_(torch.from_numpy(gS).float())
         self.st["nll_s"] = float(nll)
         self.st["iter"] += 1
+        if mode == 0:
+            dS.copy_(torch.from_numpy(gS).float())
+            return
+        # fused S-step on this shard: lambda_s S / ||S|| with the (global) norm in the state
+        nrm = math.sqrt(self.st["normsq_s"])
+        gg = torch.from_numpy(gS).float() + (lambda_s / nrm if nrm > 0 else 0.0) * S
+        self.st["step_s"] += 1
+        self._adam(S, mS, vS, gg, self.st["step_s"], adam)
+        self.st["normsq_s"] = float((S.double() ** 2).sum())  # this shard's, settled later
 
     def supdate(self, S, mS, vS, g, adam, lambda_s):
         nrm = math.sqrt(self.st["normsq_s"])
@@ -146,15 +168,24 @@ def _run(dist_mod, rank, world):
     return sol.S_pixels().reshape(R, I * J), sol.C_global(), eng.read_state()
 
 
-def _worker(rank, world, port, out_path):
+def _run_ij(dist_mod, rank, world):
+    """IJ-slab: rank g owns image rows [i0, i1) (all bins), C replicated."""
+    from quantized_spectrum_cartography_amd.distributed import IJSlabSolver, kslab_bounds
+    S0, C0, Y, Wx, b, sigma = _problem()
+    i0, i1 = kslab_bounds(I, world, rank)
+    obs = _Obs(Y[:, :, i0:i1], Wx[:, :, i0:i1])
+    eng = _CpuEngine(obs, b.numpy(), sigma)
+    sol = IJSlabSolver(obs, S0[:, :, i0:i1], C0, dist=dist_mod, engine=eng)
+    sol.run(ITERS)
+    return sol.S_pixels().reshape(R, -1), sol.C.clone(), eng.read_state()
+
+
+def _worker(rank, world, port, out_path, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        S, C, st = _run(dist, rank, world)
-        if rank == 0:
-            np.savez(out_path, S=S.numpy(), C=C.numpy(), step_s=st["step_s"])
-        else:
-            np.savez(out_path + ".r1", S=S.numpy())
+        S, C, st = (_run if mode == "k" else _run_ij)(dist, rank, world)
+        np.savez(out_path + ".r%d" % rank, S=S.numpy(), C=C.numpy(), step_s=st["step_s"])
     finally:
         dist.destroy_process_group()
 
@@ -178,10 +209,10 @@ def test_kslab_bounds_partition():
 
 
 def test_kslab_two_ranks_match_single_process(tmp_path):
-    out = str(tmp_path / "r0.npz")
-    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True,
+    out = str(tmp_path / "k")
+    mp.start_processes(_worker, args=(2, _free_port(), out, "k"), nprocs=2, join=True,
                        start_method="spawn")
-    two = np.load(out)
+    two = np.load(out + ".r0.npz")
     r1 = np.load(out + ".r1.npz")
     S1, C1, _ = _run(_SoloDist, 0, 1)
     # S is replicated: both ranks hold the same (all-reduced gradient, same update)
@@ -195,3 +226,22 @@ def test_kslab_two_ranks_match_single_process(tmp_path):
     ref = osolver.free_s_solve(S0, C0, Y, Wx, b, sigma, n_iter=ITERS)
     assert rel_fro(two["S"], ref["S"].reshape(R, -1).numpy()) < 1e-5
     assert rel_fro(two["C"], ref["C"].numpy()) < 1e-5
+
+
+def test_ijslab_two_ranks_match_single_process(tmp_path):
+    out = str(tmp_path / "ij")
+    mp.start_processes(_worker, args=(2, _free_port(), out, "ij"), nprocs=2, join=True,
+                       start_method="spawn")
+    r0, r1 = np.load(out + ".r0.npz"), np.load(out + ".r1.npz")
+    # C is replicated: both ranks hold the same (all-reduced gradient, same update)
+    assert np.array_equal(r0["C"], r1["C"])
+    assert int(r0["step_s"]) == ITERS
+    # the pixel blocks reassemble the single-process S (rows [0, I/2) and [I/2, I))
+    S_two = np.concatenate([r0["S"].reshape(R, -1, J), r1["S"].reshape(R, -1, J)], axis=1)
+    S1, C1, _ = _run_ij(_SoloDist, 0, 1)
+    assert rel_fro(S_two.reshape(R, -1), S1.numpy()) < 1e-6
+    assert rel_fro(r0["C"], C1.numpy()) < 1e-6
+    S0, C0, Y, Wx, b, sigma = _problem()
+    ref = osolver.free_s_solve(S0, C0, Y, Wx, b, sigma, n_iter=ITERS)
+    assert rel_fro(S_two.reshape(R, -1), ref["S"].reshape(R, -1).numpy()) < 1e-5
+    assert rel_fro(r0["C"], ref["C"].numpy()) < 1e-5
