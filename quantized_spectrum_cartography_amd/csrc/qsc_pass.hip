@@ -259,6 +259,15 @@ __device__ __forceinline__ float half_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// ||C||^2 in one fixed order (threads 0..255 stride 256, then the block sum): shared by the
+// C-pass (256-thread blocks) and qsc_cupdate (1024), so both give the same bits
+__device__ __forceinline__ float cnorm_sq(const float* __restrict__ C, int n, float* sh) {
+  float s2 = 0.0f;
+  if (threadIdx.x < 256)
+    for (int i = threadIdx.x; i < n; i += 256) s2 = __builtin_fmaf(C[i], C[i], s2);
+  return block_sum(s2, sh);
+}
+
 // a1 if odd else a0, as bit operations: a ternary on a lane-varying bit is turned into a
 // dynamically indexed register array (scratch) by the compiler
 __device__ __forceinline__ float pick(uint32_t oddmask, float a0, float a1) {
@@ -516,7 +525,7 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
     const E* __restrict__ ent, const int* __restrict__ width, const int64_t* __restrict__ off,
     int nks, int PT, int xcd_map, Lik lk, Edges E_, int nbins, int R, int K,
     const float* __restrict__ S, const float* __restrict__ C, float* __restrict__ slab,
-    float* __restrict__ part_nll) {
+    float* __restrict__ part_nll, float* __restrict__ cnsq) {
   using T = Ent<E>;
   using V4 = typename T::V4;
   constexpr int SP = Pitch<RP>::v;
@@ -604,6 +613,11 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
     for (int pp = 1; pp < kCParts; ++pp) a += Nl[pp];
     part_nll[wi] = a;
   }
+  if (blockIdx.x == 0) {
+    // ||C||^2 for the C update's regulariser (fixed order; C is read-only in this kernel)
+    const float nsq = cnorm_sq(C, R * K, Nl);  // Nl's slots are free again
+    if (threadIdx.x == 0) *cnsq = nsq;
+  }
   STAMP(wg, kStampLast);
   RSTAMP(wg, 29);
 }
@@ -648,48 +662,60 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
     const float* __restrict__ slab, int ntiles, int nks, int R, int K, float* __restrict__ C,
     int mode, float* __restrict__ dC, float* __restrict__ mC, float* __restrict__ vC,
     qsc_adam ad, float lambda_c, const float* __restrict__ normsq_ext,
-    qsc_state* __restrict__ st, const float* __restrict__ part_nll_c, int npart_c,
-    const float* __restrict__ part_nll_s, const float* __restrict__ part_nsq_s, int nslices,
-    float* __restrict__ hist, int hist_cap) {
+    const float* __restrict__ cnsq, qsc_state* __restrict__ st,
+    const float* __restrict__ part_nll_c, int npart_c, const float* __restrict__ part_nll_s,
+    const float* __restrict__ part_nsq_s, int nslices, float* __restrict__ hist, int hist_cap) {
   constexpr int NW = kFBlock / 64;
   __shared__ float red[NW][64];
   __shared__ float shn[NW];
   __shared__ Scalars sc;
   const int Kp = nks * 64;
-  const int r = blockIdx.x / nks, ks = blockIdx.x - r * nks;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+
+  // ||C||^2 of the C this step differentiates: written by the C-pass (C is read-only there),
+  // or the caller's global value (K-slab); never re-read here, where blocks overwrite C
+  const float nsq = normsq_ext ? *normsq_ext : *cnsq;
+
+  if (blockIdx.x == R * nks) {
+    // book-keeping block: settle the S-pass partials and total the C-pass NLL
+    settle_s(st, part_nll_s, part_nsq_s, nslices, hist, hist_cap, shn);
+    float s = 0.0f;
+    for (int i = threadIdx.x; i < npart_c; i += blockDim.x) s += part_nll_c[i];
+    const float tot = block_sum(s, shn);
+    if (threadIdx.x == 0) {
+      st->nll_c = tot;
+      if (mode == 1) {
+        st->normsq_c = nsq;
+        st->pending |= QSC_PEND_C;
+      }
+      if (mode == 2) dC[(int64_t)R * K] = st->normsq_s;  // this shard's ||S||^2 (IJ-slab)
+    }
+    return;
+  }
+
+  const int r = blockIdx.x / nks, ks = blockIdx.x - r * nks;
   const int k = ks * 64 + lane;
-
-  // tile sum: wave w takes tiles w, w+16, ...; eight independent loads in flight
-  const float* col = slab + (int64_t)r * Kp + k;
-  const int64_t tstride = (int64_t)R * Kp;
-  float a = 0.0f;
-  int tt = wave;
-  for (; tt + 7 * NW < ntiles; tt += 8 * NW) {
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = col[(int64_t)(tt + j * NW) * tstride];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) a += v[j];
-  }
-  for (; tt < ntiles; tt += NW) a += col[(int64_t)tt * tstride];
-  red[wave][lane] = a;
-
-  float nsq = 0.0f;
-  if (mode == 1 && normsq_ext == nullptr) {
-    // ||C||^2 of the current C, same fixed order in every block
-    float s2 = 0.0f;
-    for (int i = threadIdx.x; i < R * K; i += blockDim.x) s2 = __builtin_fmaf(C[i], C[i], s2);
-    nsq = block_sum(s2, shn);
-  } else {
-    __syncthreads();
-    nsq = normsq_ext ? *normsq_ext : 0.0f;
-  }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && mode == 1) {
     const float nrm = sqrtf(nsq);
     sc.coef = nrm > 0.0f ? lambda_c / nrm : 0.0f;
     sc.as = adam_scalars(ad, st->step_c + 1);
   }
+  // tile sum: wave w takes tiles w, w+16, ...; sixteen independent loads in flight per group
+  const float* col = slab + (int64_t)r * Kp + k;
+  const int64_t tstride = (int64_t)R * Kp;
+  float a = 0.0f;
+  for (int t0 = wave; t0 < ntiles; t0 += 16 * NW) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int tt = t0 + j * NW;
+      v[j] = col[(int64_t)min(tt, ntiles - 1) * tstride];
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (t0 + j * NW < ntiles) a += v[j];
+  }
+  red[wave][lane] = a;
   __syncthreads();
   if (wave == 0 && k < K) {
     float g = red[0][lane];
@@ -707,20 +733,6 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
       dC[i] = g;  // modes 0 and 2
     }
   }
-  if (blockIdx.x == 0) {
-    settle_s(st, part_nll_s, part_nsq_s, nslices, hist, hist_cap, shn);
-    float s = 0.0f;
-    for (int i = threadIdx.x; i < npart_c; i += blockDim.x) s += part_nll_c[i];
-    const float tot = block_sum(s, shn);
-    if (threadIdx.x == 0) {
-      st->nll_c = tot;
-      if (mode == 1) {
-        st->normsq_c = nsq;
-        st->pending |= QSC_PEND_C;
-      }
-      if (mode == 2) dC[(int64_t)R * K] = st->normsq_s;  // this shard's ||S||^2 (IJ-slab)
-    }
-  }
 }
 
 // C update from an externally reduced gradient g [R][K] (IJ-slab sharding, after the RCCL
@@ -735,9 +747,7 @@ __global__ void __launch_bounds__(kFBlock) cupdate_kernel(
   __shared__ float shn[NW];
   __shared__ Scalars sc;
   const int n = R * K;
-  float s2 = 0.0f;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) s2 = __builtin_fmaf(C[i], C[i], s2);
-  const float nsq = block_sum(s2, shn);
+  const float nsq = cnorm_sq(C, n, shn);
   if (threadIdx.x == 0) {
     const float nrm = sqrtf(nsq);
     sc.coef = nrm > 0.0f ? lambda_c / nrm : 0.0f;
@@ -838,9 +848,7 @@ __global__ void __launch_bounds__(kSBlock) nsq_part_kernel(const float* __restri
 __global__ void __launch_bounds__(1024) sumsq_small_kernel(const float* __restrict__ x, int n,
                                                            float* __restrict__ out) {
   __shared__ float sh[16];
-  float s = 0.0f;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) s = __builtin_fmaf(x[i], x[i], s);
-  const float r = block_sum(s, sh);
+  const float r = cnorm_sq(x, n, sh);  // the C-pass's order
   if (threadIdx.x == 0) *out = r;
 }
 
@@ -859,6 +867,7 @@ struct PassWs {
   float* snsq;      // nslices
   double* init;     // 256
   int* sched;       // S-pass queue counters [kSchedQ] + finished-wave counter (zero between launches)
+  float* cnsq;      // ||C||^2 of the C the last C-pass read (written by the C-pass)
 };
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -878,13 +887,15 @@ PassWs carve(const qsc_obs_desc* d, int R, void* ws) {
   p.init = (double*)w;
   w += al(256 * 8);
   p.sched = (int*)w;
+  w += al((kSchedQ + 1) * 4);
+  p.cnsq = (float*)w;
   return p;
 }
 
 size_t ws_bytes_for(const qsc_obs_desc* d, int R) {
   const int64_t Kp = (int64_t)d->nks * 64;
   return al((size_t)d->ntiles * R * Kp * 4) + al((size_t)d->ntiles * d->nks * 4) +
-         2 * al((size_t)(d->Pp / QSC_SLICE) * 4) + al(256 * 8) + al((kSchedQ + 1) * 4);
+         2 * al((size_t)(d->Pp / QSC_SLICE) * 4) + al(256 * 8) + al((kSchedQ + 1) * 4) + al(4);
 }
 
 bool desc_ok(const qsc_obs_desc* d) {
@@ -1051,7 +1062,7 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
 #define CPASS_LAUNCH(RPV, ET, KD, LG)                                                          \
   hipLaunchKernelGGL((cpass_kernel<RPV, ET, KD, LG>), grid, dim3(kCBlock), shm, s,           \
                      (const ET*)c_entries, c_width, c_off, d->nks, d->PT, xcd_map, lk, E,      \
-                     d->nbins, R, d->K, S, C, w.slab, w.cnll)
+                     d->nbins, R, d->K, S, C, w.slab, w.cnll, w.cnsq)
   QSC_DISPATCH_PASS(CPASS_LAUNCH);
 #undef CPASS_LAUNCH
   QSC_CHECK_LAUNCH();
@@ -1070,10 +1081,10 @@ QSC_API int qsc_cfinish(const qsc_obs_desc* d, int32_t R, float* C, int32_t mode
   PassWs w = carve(d, R, ws);
   qsc_adam ad{};
   if (adam) ad = *adam;
-  hipLaunchKernelGGL(cfinish_kernel, dim3((unsigned)(R * d->nks)), dim3(kFBlock), 0,
+  hipLaunchKernelGGL(cfinish_kernel, dim3((unsigned)(R * d->nks + 1)), dim3(kFBlock), 0,
                      STREAM(stream), w.slab, d->ntiles, d->nks, R, d->K, C, mode, dC, mC, vC, ad,
-                     lambda_c, normsq_c_ext, st, w.cnll, d->ntiles * d->nks, w.snll, w.snsq,
-                     d->Pp / QSC_SLICE, hist, hist_cap);
+                     lambda_c, normsq_c_ext, w.cnsq, st, w.cnll, d->ntiles * d->nks, w.snll,
+                     w.snsq, d->Pp / QSC_SLICE, hist, hist_cap);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }
