@@ -179,6 +179,7 @@ __device__ __forceinline__ float erf_fast(float x) {
 struct Lik {
   float a, inv_a, kgrad, offset;
   float thr;      // b[1]: the single active edge of the saturated one-bit model
+  float thr_a;    // fp32(thr / a): the one-bit model's z offset in the scaled form
 };
 
 inline Lik make_lik(const qsc_model* m) {
@@ -189,6 +190,7 @@ inline Lik make_lik(const qsc_model* m) {
   l.kgrad = p.kgrad;
   l.offset = p.offset;
   l.thr = m->nbounds >= 2 ? m->bounds[1] : 0.0f;
+  l.thr_a = (float)((double)l.thr / (double)l.a);
   return l;
 }
 
@@ -291,12 +293,17 @@ __device__ __forceinline__ f2v log2_2(f2v x) {
   return f2v{__builtin_amdgcn_logf(x.x), __builtin_amdgcn_logf(x.y)};
 }
 
-// lik_grad for two entries (t.x with code c0, t.y with code c1)
+// lik_grad for two entries (t.x with code c0, t.y with code c1).
+// Linear model (one-bit and multi-bin): the caller passes t in the SCALED form t' = -t / a
+// (its register factor vector pre-multiplied by -1/a, so the dot product yields t' directly)
+// and, for the general kind, edges pre-divided by a: z = thr/a + t', u = hi/a + t',
+// w = lo/a + t' (one add instead of a subtract and a division per entry).  The log model takes
+// t itself (x = log(t + offset) needs it).
 template <int KIND, bool LOG>
 __device__ __forceinline__ void lik_grad2(f2v t, int c0, int c1, const float2* __restrict__ edges,
                                           const Lik& c, f2v& log2P, f2v& g) {
   if (KIND == LIK_ONEBIT) {
-    const f2v z = div_lik2(splat2(c.thr) - t, c);
+    const f2v z = splat2(c.thr_a) + t;
     const f2v F = splat2(0.5f) * (splat2(1.0f) + erf_fast2(z));
     const f2v Fc = splat2(1.0f) - F;
     const bool z0 = (c0 == 0), z1 = (c1 == 0);
@@ -306,15 +313,18 @@ __device__ __forceinline__ void lik_grad2(f2v t, int c0, int c1, const float2* _
     g = f2v{z0 ? e.x : -e.x, z1 ? e.y : -e.y} * rp;
     log2P = log2_2(P);
   } else {
-    f2v x = t, tinv = splat2(1.0f);
+    const float2 e0 = edges[c0], e1 = edges[c1];
+    f2v u, w, tinv = splat2(1.0f);
     if (LOG) {
       const f2v tp = t + splat2(c.offset);
-      x = f2v{logf(tp.x), logf(tp.y)};
+      const f2v x = f2v{logf(tp.x), logf(tp.y)};
       tinv = rcp2(tp);
+      u = div_lik2(f2v{e0.y, e1.y} - x, c);
+      w = div_lik2(f2v{e0.x, e1.x} - x, c);
+    } else {
+      u = f2v{e0.y, e1.y} + t;
+      w = f2v{e0.x, e1.x} + t;
     }
-    const float2 e0 = edges[c0], e1 = edges[c1];
-    const f2v u = div_lik2(f2v{e0.y, e1.y} - x, c);
-    const f2v w = div_lik2(f2v{e0.x, e1.x} - x, c);
     const f2v P = splat2(0.5f) * (splat2(1.0f) + erf_fast2(u)) -
                   splat2(0.5f) * (splat2(1.0f) + erf_fast2(w));
     const f2v d = (exp2_2(u * u * splat2(kNegLog2e)) - exp2_2(w * w * splat2(kNegLog2e))) *

@@ -28,7 +28,10 @@ namespace {
 
 constexpr int kSBlock = 256;   // S-pass / S-update: 4 waves = 4 slices of QSC_SLICE pixels
 constexpr int kSWaves = kSBlock / 64;
-constexpr int kCBlock = 256;   // C-pass: 4 waves = 4 quarters of one (tile, 64-bin slice)
+#ifndef QSC_CPASS_BLOCK
+#define QSC_CPASS_BLOCK 512
+#endif
+constexpr int kCBlock = QSC_CPASS_BLOCK;  // C-pass: kCBlock/64 waves = parts of one (tile, 64-bin slice)
 constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 
 // occupancy targets (waves per SIMD) that bound the register allocation of the passes; the
@@ -365,6 +368,8 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     float* __restrict__ part_nll, float* __restrict__ part_nsq, int* __restrict__ sched) {
   constexpr int CP = Pitch<RP>::v;
   constexpr int RH = RP / 2;  // row elements updated per lane (half row)
+  // linear models evaluate the entries in the scaled form t' = -t/a (lik_grad2)
+  const float own_scale = LOG ? 1.0f : -lk.inv_a;
   // all LDS carved from the 16-B aligned dynamic region (no statics ahead of it)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   Scalars& sc = *reinterpret_cast<Scalars*>(smem);            // 32 B reserved
@@ -398,13 +403,20 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
   float c0[RP];
 #pragma unroll
   for (int r = 0; r < RP; ++r) c0[r] = C[(int64_t)min(r, R - 1) * K + min(k0, K - 1)];
+  const float2 e0 = E_.e[min(k0, nbins - 1)];
+  __builtin_amdgcn_sched_barrier(0);
   SliceIn<RP, E, ADAM> cur;
-  if (s < nslices) slice_load(cur, ent, width, off, s, p, h, S, mS, vS);
+  // unconditional (a wave without slices reads slice 0): a static load count lets the C^T
+  // staging below wait for its own reads only
+  slice_load(cur, ent, width, off, s < nslices ? s : 0, p, h, S, mS, vS);
   // 2. stage C^T (rows padded to CP) and the bin edges in LDS
-  if (k0 < K) {
+  {
+    // branch-free (threads past K rewrite row K-1 with its own values), so the C^T reads stay
+    // ahead of the slice reads
+    const int kw = min(k0, K - 1);
 #pragma unroll
     for (int r = 0; r < RP; r += 4)
-      *reinterpret_cast<float4*>(Cl + k0 * CP + r) =
+      *reinterpret_cast<float4*>(Cl + kw * CP + r) =
           make_float4(r < R ? c0[r] : 0.0f, r + 1 < R ? c0[r + 1] : 0.0f,
                       r + 2 < R ? c0[r + 2] : 0.0f, r + 3 < R ? c0[r + 3] : 0.0f);
   }
@@ -416,7 +428,8 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     for (int r = 0; r < RP; r += 4)
       *reinterpret_cast<float4*>(Cl + k * CP + r) = make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
   }
-  for (int b = threadIdx.x; b < nbins; b += kSBlock) El[b] = E_.e[b];
+  El[min(k0, nbins - 1)] = e0;  // branch-free like C^T
+  for (int b = k0 + kSBlock; b < nbins; b += kSBlock) El[b] = E_.e[b];
   if (threadIdx.x == 0) {
     if (ADAM) {
       const float nrm = sqrtf(st->normsq_s);
@@ -451,7 +464,7 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     for (int r = 0; r < RP; ++r) sv[r] = cur.sv[r];
     f2v own[RP / 2];
 #pragma unroll
-    for (int j = 0; j < RP / 2; ++j) own[j] = f2v{sv[2 * j], sv[2 * j + 1]};
+    for (int j = 0; j < RP / 2; ++j) own[j] = f2v{sv[2 * j], sv[2 * j + 1]} * splat2(own_scale);
 
     // 4. likelihood + gradient over the pixel's observed entries
     f2v accp[RP / 2];
@@ -510,7 +523,7 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
 // ---------------------------------------------------------------------------------------
 // C-pass
 // ---------------------------------------------------------------------------------------
-// One workgroup per (pixel tile, 64-bin frequency slice): 4 waves, each walking a quarter of
+// One workgroup per (pixel tile, 64-bin frequency slice): kCParts waves, each walking a part of
 // the slice's per-bin entry lists (lane = bin k) against the tile's S rows staged in LDS.
 // Small workgroups (several resident per CU, dispatched as others retire) let the hardware
 // balance the uneven lists and overlap one group's staging with another's arithmetic.  The
@@ -550,7 +563,7 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   STAMP(wg, 0);
   RSTAMP(wg, 28);
 
-  // 1. entry read-ahead of this wave's quarter of the lists and C[:, k], before the staging
+  // 1. entry read-ahead of this wave's part of the lists and C[:, k], before the staging
   const int64_t wi = (int64_t)t * nks + ks;
   const int W4 = width[wi] >> 2;
   const int j0 = (W4 * part) / kCParts, j1 = (W4 * (part + 1)) / kCParts;
@@ -577,12 +590,13 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   __syncthreads();
   STAMP(wg, 1);
 
-  // 3. likelihood + gradient over the quarter lists
+  // 3. likelihood + gradient over the part lists
+  const float own_scale = LOG ? 1.0f : -lk.inv_a;  // scaled form t' = -t/a (lik_grad2)
   f2v own[RP / 2];
 #pragma unroll
   for (int j = 0; j < RP / 2; ++j)
     own[j] = f2v{(2 * j < R && k < K) ? cv[2 * j] : 0.0f,
-                 (2 * j + 1 < R && k < K) ? cv[2 * j + 1] : 0.0f};
+                 (2 * j + 1 < R && k < K) ? cv[2 * j + 1] : 0.0f} * splat2(own_scale);
   f2v accp[RP / 2];
 #pragma unroll
   for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
@@ -599,7 +613,7 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   __syncthreads();
   STAMP(wg, 3);
 
-  // 4. fixed-order sum of the quarters -> slab rows of this tile / slice
+  // 4. fixed-order sum of the parts -> slab rows of this tile / slice
   for (int i = threadIdx.x; i < R * 64; i += kCBlock) {
     float a = Pl[i];
 #pragma unroll
@@ -906,6 +920,12 @@ bool desc_ok(const qsc_obs_desc* d) {
 
 int rp_of(int R) { return R <= 4 ? 4 : (R <= 8 ? 8 : 16); }
 
+// linear model edges pre-divided by a for the scaled entry form (lik_grad2)
+void scale_edges(Edges* E, int nbins, float a) {
+  for (int c = 0; c < nbins; ++c)
+    E->e[c] = make_float2((float)((double)E->e[c].x / a), (float)((double)E->e[c].y / a));
+}
+
 // compute units of the current device (cached per device id)
 int cu_count() {
   static int cached[64] = {0};
@@ -1016,6 +1036,7 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
   make_edges(m, &E);
   const Lik lk = make_lik(m);
   const int kind = lik_kind(m);
+  if (!m->log_model) scale_edges(&E, m->nbounds - 1, lk.a);
   const int nslices = d->Pp / QSC_SLICE;
   const int bpc = std::min(QSC_SPASS_BPC, RP >= 8 ? 2 : QSC_SPASS_WAVES);
   const dim3 grid((unsigned)std::min<int64_t>(ceil_div(nslices, kSWaves), (int64_t)cu_count() * bpc));
@@ -1056,6 +1077,7 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
   make_edges(m, &E);
   const Lik lk = make_lik(m);
   const int kind = lik_kind(m);
+  if (!m->log_model) scale_edges(&E, m->nbounds - 1, lk.a);
   hipStream_t s = STREAM(stream);
   const int xcd_map = (d->ntiles % 8) == 0 ? 1 : 0;
   const dim3 grid((unsigned)((int64_t)d->ntiles * d->nks));

@@ -31,13 +31,13 @@ def cpass_timeline(sol, _lib, ctypes):
     print("  start", pct_us(st[:, 28] - r0))
     print("  end  ", pct_us(st[:, 29] - r0))
     print("  staging+barrier", pct(st[:, 1] - st[:, 0]))
-    ok = st[:, 2] > 0
-    print("  walk (waves with a unit)", pct(st[ok, 2] - st[ok, 1]))
-    print("  to LDS partials", pct(st[:, 3] - np.where(ok, st[:, 2], st[:, 1])))
-    ok4 = st[:, 4] > 0
-    if ok4.any():
-        print("  barrier wait", pct(st[ok4, 4] - st[ok4, 3]))
-        print("  reduce+slab", pct(st[ok4, 31] - st[ok4, 4]))
+    print("  walk            ", pct(st[:, 2] - st[:, 1]))
+    print("  partials+barrier", pct(st[:, 3] - st[:, 2]))
+    print("  reduce+slab     ", pct(st[:, 31] - st[:, 3]))
+    life = (st[:, 29] - st[:, 28]) / 100.0
+    print("  wave lifetime   ", pct_us(st[:, 29] - st[:, 28]))
+    print("  concurrency: sum(lifetimes)/span/waves-per-CU-capacity: %.2f waves resident on average per CU" % (
+        life.sum() / ((st[:, 29].max() - r0) / 100.0) / 256))
 
 
 def main():
