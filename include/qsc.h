@@ -108,6 +108,10 @@ typedef struct qsc_state {
  *  C-format ("frequency slices" per pixel tile): tile t (PT positions), k-slice ks (64 k's),
  *     lane l (k = 64*ks + l), entry j < c_width[t*nks+ks]:
  *     idx = c_off[t*nks+ks] + (j/4)*256 + l*4 + (j%4);  value = qlocal | code << QBITS
+ *     Tile rows are whole S-format slices dealt in snake order, so that every tile holds the
+ *     same mix of dense and sparse positions (positions are count-sorted): row qlocal of tile t
+ *     is position  g*QSC_SLICE + qlocal%QSC_SLICE,  g = i*ntiles + (i odd ? ntiles-1-t : t),
+ *     i = qlocal/QSC_SLICE.
  *  narrow (wide == 0): uint16 entries, KBITS = QBITS = 12, code PAD = 15 (K, PT <= 4096, nbins <= 15)
  *  wide   (wide == 1): uint32 entries, KBITS = QBITS = 24, code PAD = 255 */
 typedef struct qsc_obs_desc {

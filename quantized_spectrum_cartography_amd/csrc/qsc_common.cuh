@@ -334,6 +334,100 @@ __device__ __forceinline__ void lik_grad2(f2v t, int c0, int c1, const float2* _
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Four-entry forms: the same per-element operation sequence as lik_grad2 (bitwise the same
+// results) on 4-wide vectors, which the backend splits into two independent v_pk_* chains.
+// Interleaving the two chains fills the issue slot that a dependent packed op would otherwise
+// spend on an s_nop (packed-VALU read-after-write hazard) and doubles the ILP per wave.
+// ------------------------------------------------------------------------------------
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4v fma4(f4v a, f4v b, f4v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f4v splat4(float x) { return f4v{x, x, x, x}; }
+__device__ __forceinline__ f4v exp2_4(f4v x) {
+  return f4v{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y), __builtin_amdgcn_exp2f(x.z),
+             __builtin_amdgcn_exp2f(x.w)};
+}
+__device__ __forceinline__ f4v rcp4(f4v x) {
+  return f4v{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y), __builtin_amdgcn_rcpf(x.z),
+             __builtin_amdgcn_rcpf(x.w)};
+}
+__device__ __forceinline__ f4v log2_4(f4v x) {
+  return f4v{__builtin_amdgcn_logf(x.x), __builtin_amdgcn_logf(x.y), __builtin_amdgcn_logf(x.z),
+             __builtin_amdgcn_logf(x.w)};
+}
+__device__ __forceinline__ f4v sel4(bool c0, bool c1, bool c2, bool c3, f4v a, f4v b) {
+  return f4v{c0 ? a.x : b.x, c1 ? a.y : b.y, c2 ? a.z : b.z, c3 ? a.w : b.w};
+}
+
+__device__ __forceinline__ f4v erf_fast4(f4v x) {
+  const f4v ax = __builtin_elementwise_abs(x);
+  f4v p = fma4(ax, splat4(bits(0x378e98abu)), splat4(bits(0xb9c68948u)));
+  p = fma4(ax, p, splat4(bits(0x3b7cd369u)));
+  p = fma4(ax, p, splat4(bits(0xbcc618b2u)));
+  p = fma4(ax, p, splat4(bits(0x3dda74e4u)));
+  p = fma4(ax, p, splat4(bits(0x3f228afdu)));
+  p = fma4(ax, p, splat4(bits(0x3e03c728u)));
+  p = fma4(ax, p, ax);
+  const f4v pe = p * splat4(bits(0xbfb8aa3bu));
+  const f4v big = splat4(1.0f) - exp2_4(pe);
+  const f4v t = x * x;
+  f4v q = fma4(splat4(bits(0xba1345e1u)), t, splat4(bits(0x3ba10414u)));
+  q = fma4(t, q, splat4(bits(0xbcdac9b8u)));
+  q = fma4(t, q, splat4(bits(0x3de703beu)));
+  q = fma4(t, q, splat4(bits(0xbec09330u)));
+  q = fma4(t, q, splat4(bits(0x3e0375d0u)));
+  const f4v small = fma4(ax, q, ax);
+  return f4v{__builtin_copysignf(ax.x < 1.0f ? small.x : big.x, x.x),
+             __builtin_copysignf(ax.y < 1.0f ? small.y : big.y, x.y),
+             __builtin_copysignf(ax.z < 1.0f ? small.z : big.z, x.z),
+             __builtin_copysignf(ax.w < 1.0f ? small.w : big.w, x.w)};
+}
+
+__device__ __forceinline__ f4v div_lik4(f4v x, const Lik& c) {
+  const f4v ia = splat4(c.inv_a);
+  const f4v q = x * ia;
+  const f4v r = fma4(-q, splat4(c.a), x);
+  return fma4(r, ia, q);
+}
+
+// lik_grad2 on four entries (codes c[0..3]); same scaled-form convention
+template <int KIND, bool LOG>
+__device__ __forceinline__ void lik_grad4(f4v t, const int (&cd)[4],
+                                          const float2* __restrict__ edges, const Lik& c,
+                                          f4v& log2P, f4v& g) {
+  if (KIND == LIK_ONEBIT) {
+    const f4v z = splat4(c.thr_a) + t;
+    const f4v F = splat4(0.5f) * (splat4(1.0f) + erf_fast4(z));
+    const f4v Fc = splat4(1.0f) - F;
+    const bool z0 = (cd[0] == 0), z1 = (cd[1] == 0), z2 = (cd[2] == 0), z3 = (cd[3] == 0);
+    const f4v P = sel4(z0, z1, z2, z3, F, Fc);
+    const f4v e = exp2_4(z * z * splat4(kNegLog2e)) * splat4(c.kgrad);
+    const f4v rp = rcp4(P);
+    g = sel4(z0, z1, z2, z3, e, -e) * rp;
+    log2P = log2_4(P);
+  } else {
+    const float2 e0 = edges[cd[0]], e1 = edges[cd[1]], e2 = edges[cd[2]], e3 = edges[cd[3]];
+    f4v u, w, tinv = splat4(1.0f);
+    if (LOG) {
+      const f4v tp = t + splat4(c.offset);
+      const f4v x = f4v{logf(tp.x), logf(tp.y), logf(tp.z), logf(tp.w)};
+      tinv = rcp4(tp);
+      u = div_lik4(f4v{e0.y, e1.y, e2.y, e3.y} - x, c);
+      w = div_lik4(f4v{e0.x, e1.x, e2.x, e3.x} - x, c);
+    } else {
+      u = f4v{e0.y, e1.y, e2.y, e3.y} + t;
+      w = f4v{e0.x, e1.x, e2.x, e3.x} + t;
+    }
+    const f4v P = splat4(0.5f) * (splat4(1.0f) + erf_fast4(u)) -
+                  splat4(0.5f) * (splat4(1.0f) + erf_fast4(w));
+    const f4v d = (exp2_4(u * u * splat4(kNegLog2e)) - exp2_4(w * w * splat4(kNegLog2e))) *
+                  splat4(c.kgrad);
+    g = d * rcp4(P) * tinv;
+    log2P = log2_4(P);
+  }
+}
+
 // One observed entry end to end: t is the linear reconstruction value; returns P and the
 // gradient of -log P w.r.t. t (chain rule through log(t + offset) in the log model).
 __device__ __forceinline__ void entry_grad(float t, int code, const float2* edges,
@@ -380,6 +474,14 @@ __device__ __forceinline__ T block_sum(T v, T* sh) {
 
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 __host__ __device__ inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
+
+// Position of row ql of C-format pixel tile t (include/qsc.h): whole slices dealt to the nt
+// tiles in snake order, so that every tile carries the same mix of the count-sorted positions.
+__host__ __device__ inline int64_t tile_pos(int t, int ql, int nt) {
+  const int i = ql / QSC_SLICE;
+  const int g = i * nt + ((i & 1) ? (nt - 1 - t) : t);
+  return (int64_t)g * QSC_SLICE + (ql % QSC_SLICE);
+}
 
 // Adam bias corrections exactly as torch.optim.Adam (_single_tensor_adam) forms them in
 // Python double precision, then hands them to fp32 tensor-scalar ops.

@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(kBlock) c_width_kernel(const uint8_t* __restri
   for (int i = threadIdx.x; i < nks * 64; i += blockDim.x) lcnt[i] = 0;
   __syncthreads();
   for (int ql = threadIdx.x; ql < PT; ql += blockDim.x) {
-    const int p = perm[(int64_t)t * PT + ql];
+    const int p = perm[tile_pos(t, ql, gridDim.x)];  // grid = one block per tile
     if (p < 0 || p >= P) continue;
     for (int k = 0; k < K; ++k)
       if (codes[(int64_t)k * P + p] != QSC_UNOBSERVED) atomicAdd(&lcnt[k], 1);
@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(kBlock) c_fill_kernel(const uint8_t* __restric
     int j = 0;
     if (kk < K) {
       for (int ql = 0; ql < PT; ++ql) {
-        const int p = perm[(int64_t)t * PT + ql];
+        const int p = perm[tile_pos(t, ql, gridDim.x)];  // grid = one block per tile
         if (p < 0 || p >= P) continue;
         const uint8_t c = codes[(int64_t)kk * P + p];
         if (c != QSC_UNOBSERVED)

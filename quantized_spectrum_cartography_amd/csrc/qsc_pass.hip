@@ -46,11 +46,14 @@ template <int RP, int W>
 struct Occ {
   static constexpr int v = (RP > 8) ? (W > 4 ? 4 : W) : W;
 };
-// the persistent S-pass holds two slices' inputs in registers: ranks 8 and 16 get 256 VGPRs
-// (2 waves per SIMD, the resident grid of QSC_SPASS_BPC = 2)
+// the persistent S-pass holds two slices' inputs in registers: rank 16 gets 256 VGPRs (2 waves
+// per SIMD), rank 8 fits 128 (QSC_SPASS_BPC8 = 3 resident blocks: measured fastest of 2, 3, 4)
+#ifndef QSC_SPASS_BPC8
+#define QSC_SPASS_BPC8 3  // resident S-pass blocks per CU at rank 8 (3 waves per SIMD)
+#endif
 template <int RP, int EB, int W>
 struct OccS {
-  static constexpr int v = (RP >= 8) ? (W > 2 ? 2 : W) : W;
+  static constexpr int v = (RP > 8) ? (W > 2 ? 2 : W) : (RP == 8) ? QSC_SPASS_BPC8 : W;
 };
 
 // LDS row pitch (floats) of an RP-float gathered row: 16-B aligned for ds_read_b128 and, for
@@ -122,14 +125,44 @@ template <int RP, typename E, int KIND, bool LOG>
 __device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const f2v (&own)[RP / 2],
                                       const float* __restrict__ tab,
                                       const float2* __restrict__ edges, const Lik& lk,
-                                      f2v (&acc)[RP / 2], float& nll) {
+                                      f2v (&acc)[RP / 2], float& nll, bool valid = true) {
   using T = Ent<E>;
   uint32_t e[4];
   T::unpack(v, e);
+#if QSC_CHUNK4
+  // all four entries at once: four gathers in flight, then the per-entry math as two
+  // interleaved packed chains (lik_grad4); sums in the same order as the pairwise form
+  {
+    int cd[4];
+    bool pd[4];
+    f2v o[4][RP / 2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int cu = (int)(e[u] >> T::kBits);
+      pd[u] = (cu == T::kPad) || !valid;
+      cd[u] = pd[u] ? 0 : cu;
+      lds_row2<RP>(tab + (e[u] & T::kMask) * Pitch<RP>::v, o[u]);
+    }
+    const f4v t = f4v{dot2<RP>(own, o[0]), dot2<RP>(own, o[1]), dot2<RP>(own, o[2]),
+                      dot2<RP>(own, o[3])};
+    f4v log2P, g;
+    lik_grad4<KIND, LOG>(t, cd, edges, lk, log2P, g);
+    const float gu[4] = {pd[0] ? 0.0f : g.x, pd[1] ? 0.0f : g.y, pd[2] ? 0.0f : g.z,
+                         pd[3] ? 0.0f : g.w};
+    nll -= (pd[0] ? 0.0f : log2P.x) + (pd[1] ? 0.0f : log2P.y);
+    nll -= (pd[2] ? 0.0f : log2P.z) + (pd[3] ? 0.0f : log2P.w);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int j = 0; j < RP / 2; ++j) acc[j] = fma2(splat2(gu[u]), o[u][j], acc[j]);
+    }
+    return;
+  }
+#endif
 #pragma unroll
   for (int u = 0; u < 4; u += 2) {
     const int ca = (int)(e[u] >> T::kBits), cb = (int)(e[u + 1] >> T::kBits);
-    const bool pa = (ca == T::kPad), pb = (cb == T::kPad);
+    const bool pa = (ca == T::kPad) || !valid, pb = (cb == T::kPad) || !valid;
     f2v oa[RP / 2], ob[RP / 2];
 #if QSC_DIAG_NOLDS  // diagnostic build: no gather (bounds the LDS share of the pass)
 #pragma unroll
@@ -200,6 +233,47 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
 #pragma unroll
     for (int i = 0; i < kGroup; ++i) b[i] = nb[i];
     jb = jn;
+  }
+}
+
+// Uniform-control form of walk_groups: every chunk of a group is evaluated (a chunk past the
+// lane's list end reads its clamped last chunk and is masked), so the group is one basic block
+// the compiler schedules as a whole (LDS gathers of later chunks under earlier chunks' math),
+// and the loop trip count depends only on wave-uniform values: `ju` is the smallest first
+// chunk of the wave's lanes, `j1` the (uniform) list end.  The next group is read only when
+// some lane needs it.
+template <int RP, typename E, int KIND, bool LOG>
+__device__ __forceinline__ void walk_masked(const typename Ent<E>::V4* __restrict__ src, int row,
+                                            int jb, int ju, int j1, int js,
+                                            typename Ent<E>::V4 (&b)[kGroup],
+                                            const f2v (&own)[RP / 2],
+                                            const float* __restrict__ tab,
+                                            const float2* __restrict__ edges, const Lik& lk,
+                                            f2v (&acc)[RP / 2], float& nll) {
+  using V4 = typename Ent<E>::V4;
+  j1 = __builtin_amdgcn_readfirstlane(j1);
+  ju = __builtin_amdgcn_readfirstlane(ju);
+  const int jlast = max(j1 - 1, 0);
+  // The last group is evaluated on a path that issues no loads, so the compiler's (path-
+  // insensitive) wait-count bookkeeping sees no read pending after the walk and the caller's
+  // next-slice read-ahead stays in flight through the epilogue.
+  for (;;) {
+    const int jn = jb + kGroup * js, jun = ju + kGroup * js;
+    if (jun >= j1) {  // uniform
+#pragma unroll
+      for (int i = 0; i < kGroup; ++i)
+        chunk<RP, E, KIND, LOG>(b[i], own, tab, edges, lk, acc, nll, jb + i * js < j1);
+      break;
+    }
+    V4 nb[kGroup];
+    load_group(src, row, jn, js, jlast, nb);
+#pragma unroll
+    for (int i = 0; i < kGroup; ++i)
+      chunk<RP, E, KIND, LOG>(b[i], own, tab, edges, lk, acc, nll, jb + i * js < j1);
+#pragma unroll
+    for (int i = 0; i < kGroup; ++i) b[i] = nb[i];
+    jb = jn;
+    ju = jun;
   }
 }
 
@@ -471,8 +545,13 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     float nll = 0.0f;
+#if QSC_SPASS_MASKED
+    walk_masked<RP, E, KIND, LOG>(cur.src, QSC_SLICE, h, 0, cur.j1, 2, cur.buf, own, Cl, El, lk,
+                                  accp, nll);
+#else
     walk_groups<RP, E, KIND, LOG>(cur.src, QSC_SLICE, h, cur.j1, 2, cur.buf, own, Cl, El, lk,
                                   accp, nll);
+#endif
     STAMP(w, 3 + 3 * i);
     // the two lane halves' partial dS: v_permlane32_swap (VALU) instead of an LDS shuffle
     float acc[RP];
@@ -556,7 +635,6 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
     t = blockIdx.x / nks;
     ks = blockIdx.x - t * nks;
   }
-  const int64_t q0 = (int64_t)t * PT;
   const int Kp = nks * 64;
   const int part = threadIdx.x >> 6, lane = threadIdx.x & 63;
   [[maybe_unused]] const int wg = blockIdx.x * kCParts + part;  // (diagnostic stamps)
@@ -575,15 +653,17 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
 #pragma unroll
   for (int r = 0; r < RP; ++r) cv[r] = C[(int64_t)min(r, R - 1) * K + min(k, K - 1)];
 
-  // 2. stage the pixel tile: its position rows are contiguous in [Pp][RP]; 16-B reads and
-  //    16-B LDS writes at the padded pitch SP
+  // 2. stage the pixel tile: its rows are whole position slices (qsc_tile_pos, snake-dealt),
+  //    each a contiguous run of QSC_SLICE rows in [Pp][RP]; 16-B reads and 16-B LDS writes at
+  //    the padded pitch SP
   {
-    const float4* __restrict__ src4 = reinterpret_cast<const float4*>(S + q0 * RP);
+    const float4* __restrict__ src4 = reinterpret_cast<const float4*>(S);
     constexpr int V = RP / 4;  // float4 per row
+    const int nt = gridDim.x / nks;
 #pragma unroll 4
     for (int i = threadIdx.x; i < PT * V; i += kCBlock) {
       const int ql = i / V, c = i - ql * V;
-      *reinterpret_cast<float4*>(Sl + ql * SP + 4 * c) = src4[i];
+      *reinterpret_cast<float4*>(Sl + ql * SP + 4 * c) = src4[tile_pos(t, ql, nt) * V + c];
     }
   }
   for (int i = threadIdx.x; i < nbins; i += kCBlock) El[i] = E_.e[i];
@@ -601,7 +681,11 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
 #pragma unroll
   for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
   float nll = 0.0f;
+#if QSC_CPASS_MASKED
+  walk_masked<RP, E, KIND, LOG>(src, 64, j0, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+#else
   walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+#endif
   STAMP(wg, 2);
   nll = wave_sum_dpp(nll) * kLn2;
 #pragma unroll
@@ -634,6 +718,147 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   }
   STAMP(wg, kStampLast);
   RSTAMP(wg, 29);
+}
+
+// ---------------------------------------------------------------------------------------
+// C-pass, tile form: one workgroup per pixel tile covering ALL of its k-slices, so the tile's
+// S rows are staged in LDS once (not once per 64-bin slice) and the whole grid is resident in
+// one round (tiles hold equal mixes of dense and sparse positions, qsc_tile_pos, so the
+// workgroups carry equal work).  The NW = blockDim/64 waves take units (k-slice ks, part of
+// NP) u = w, w + NW, ...: lane = bin k walks part `part` of the bin's list.  With NP = 1 a
+// unit's dC goes straight from registers to the slab; otherwise the NP parts are summed in
+// LDS in a fixed order (bitwise deterministic; no atomics).
+// ---------------------------------------------------------------------------------------
+constexpr int kCTBlock = 1024;
+
+template <int RP, typename E, int KIND, bool LOG>
+__global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
+    const E* __restrict__ ent, const int* __restrict__ width, const int64_t* __restrict__ off,
+    int nks, int NP, int PT, Lik lk, Edges E_, int nbins, int R, int K,
+    const float* __restrict__ S, const float* __restrict__ C, float* __restrict__ slab,
+    float* __restrict__ part_nll, float* __restrict__ cnsq) {
+  using T = Ent<E>;
+  using V4 = typename T::V4;
+  constexpr int SP = Pitch<RP>::v;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int NW = blockDim.x >> 6;
+  const int U = nks * NP;
+  float* Sl = smem;                                              // [PT][SP]
+  float2* El = reinterpret_cast<float2*>(Sl + (size_t)PT * SP);   // [nbins] (<= 254)
+  float* Pl = Sl + (size_t)PT * SP + 2 * 256;                     // [U][R][64]   (NP > 1)
+  float* Nl = Pl + (NP > 1 ? (size_t)U * R * 64 : 0);             // [U] / [NW]
+  const int t = blockIdx.x;
+  const int Kp = nks * 64;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const float own_scale = LOG ? 1.0f : -lk.inv_a;  // scaled form t' = -t/a (lik_grad2)
+  [[maybe_unused]] const int wg = blockIdx.x * (kCTBlock / 64) + w;  // (diagnostic stamps)
+  STAMP(wg, 0);
+  RSTAMP(wg, 28);
+
+  // 1. read-ahead of the first unit's entries and C column, ahead of the staging
+  int u = w;
+  V4 buf[kGroup];
+  float cv[RP];
+  int wi = 0, j0 = 0, j1 = 0;
+  const V4* src = nullptr;
+  auto unit_begin = [&](int uu) {
+    const int ks = uu / NP, part = uu - ks * NP;
+    wi = t * nks + ks;
+    const int W4 = width[wi] >> 2;
+    j0 = (W4 * part) / NP;
+    j1 = (W4 * (part + 1)) / NP;
+    src = reinterpret_cast<const V4*>(ent + off[wi]) + lane;
+    load_group(src, 64, j0, 1, max(j1 - 1, 0), buf);
+    const int k = ks * 64 + lane;
+#pragma unroll
+    for (int r = 0; r < RP; ++r) cv[r] = C[(int64_t)min(r, R - 1) * K + min(k, K - 1)];
+  };
+  if (u < U) unit_begin(u);
+
+  // 2. stage the pixel tile (whole position slices, 16-B reads / writes at pitch SP)
+  {
+    const float4* __restrict__ src4 = reinterpret_cast<const float4*>(S);
+    constexpr int V = RP / 4;  // float4 per row
+    const int nt = gridDim.x;
+#pragma unroll 4
+    for (int i = threadIdx.x; i < PT * V; i += blockDim.x) {
+      const int ql = i / V, c = i - ql * V;
+      *reinterpret_cast<float4*>(Sl + ql * SP + 4 * c) = src4[tile_pos(t, ql, nt) * V + c];
+    }
+  }
+  for (int i = threadIdx.x; i < nbins; i += blockDim.x) El[i] = E_.e[i];
+  __syncthreads();
+  STAMP(wg, 1);
+
+  // 3. units: likelihood + gradient over the part lists
+  for (; u < U; u += NW) {
+    const int ks = u / NP;
+    const int k = ks * 64 + lane;
+    f2v own[RP / 2];
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j)
+      own[j] = f2v{(2 * j < R && k < K) ? cv[2 * j] : 0.0f,
+                   (2 * j + 1 < R && k < K) ? cv[2 * j + 1] : 0.0f} * splat2(own_scale);
+    f2v accp[RP / 2];
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
+    float nll = 0.0f;
+    walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+    nll = wave_sum_dpp(nll) * kLn2;
+    if (NP == 1) {
+      // the unit is the whole (tile, k-slice): its slab rows straight from registers
+#pragma unroll
+      for (int j = 0; j < RP / 2; ++j) {
+        if (2 * j < R) slab[((int64_t)t * R + 2 * j) * Kp + k] = accp[j].x;
+        if (2 * j + 1 < R) slab[((int64_t)t * R + 2 * j + 1) * Kp + k] = accp[j].y;
+      }
+      if (lane == 0) part_nll[wi] = nll;
+    } else {
+#pragma unroll
+      for (int j = 0; j < RP / 2; ++j) {
+        if (2 * j < R) Pl[((size_t)u * R + 2 * j) * 64 + lane] = accp[j].x;
+        if (2 * j + 1 < R) Pl[((size_t)u * R + 2 * j + 1) * 64 + lane] = accp[j].y;
+      }
+      if (lane == 0) Nl[u] = nll;
+    }
+    if (u + NW < U) unit_begin(u + NW);
+  }
+  STAMP(wg, 2);
+
+  // 4. fixed-order sum of the parts -> slab rows of this tile (NP > 1)
+  if (NP > 1) {
+    __syncthreads();
+    STAMP(wg, 3);
+    for (int i = threadIdx.x; i < nks * R * 64; i += blockDim.x) {
+      const int ks = i / (R * 64), rl = i - ks * (R * 64);
+      const float* p = Pl + (size_t)ks * NP * R * 64 + rl;
+      float a = p[0];
+      for (int pp = 1; pp < NP; ++pp) a += p[(size_t)pp * R * 64];
+      const int r = rl >> 6, l = rl & 63;
+      slab[((int64_t)t * R + r) * Kp + ks * 64 + l] = a;
+    }
+    for (int ks = threadIdx.x; ks < nks; ks += blockDim.x) {
+      float a = Nl[ks * NP];
+      for (int pp = 1; pp < NP; ++pp) a += Nl[ks * NP + pp];
+      part_nll[t * nks + ks] = a;
+    }
+  }
+  if (blockIdx.x == 0) {
+    // ||C||^2 for the C update's regulariser (fixed order; C is read-only in this kernel)
+    __syncthreads();
+    const float nsq = cnorm_sq(C, R * K, Nl);  // Nl's slots are free again
+    if (threadIdx.x == 0) *cnsq = nsq;
+  }
+  STAMP(wg, kStampLast);
+  RSTAMP(wg, 29);
+}
+
+// LDS bytes of cpass_tile_kernel
+size_t cpass_tile_lds(int PT, int R, int nks, int NP) {
+  const int RP = R <= 4 ? 4 : (R <= 8 ? 8 : 16);
+  const size_t U = (size_t)nks * NP;
+  return (size_t)PT * (RP == 4 ? 4 : RP + 4) * 4 + 2 * 256 * 4 +
+         (NP > 1 ? U * R * 64 * 4 : 0) + std::max<size_t>(U, 16) * 4;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1038,7 +1263,7 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
   const int kind = lik_kind(m);
   if (!m->log_model) scale_edges(&E, m->nbounds - 1, lk.a);
   const int nslices = d->Pp / QSC_SLICE;
-  const int bpc = std::min(QSC_SPASS_BPC, RP >= 8 ? 2 : QSC_SPASS_WAVES);
+  const int bpc = RP > 8 ? 2 : RP == 8 ? QSC_SPASS_BPC8 : QSC_SPASS_BPC;
   const dim3 grid((unsigned)std::min<int64_t>(ceil_div(nslices, kSWaves), (int64_t)cu_count() * bpc));
   qsc_adam ad{};
   if (adam) ad = *adam;
@@ -1079,6 +1304,32 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
   const int kind = lik_kind(m);
   if (!m->log_model) scale_edges(&E, m->nbounds - 1, lk.a);
   hipStream_t s = STREAM(stream);
+#ifndef QSC_CPASS_TILE
+#define QSC_CPASS_TILE 1
+#endif
+  if (QSC_CPASS_TILE) {
+    // tile form: up to 16 waves per tile; parts per bin list while a part keeps >= 3 chunks
+#ifndef QSC_CTILE_MAXW
+#define QSC_CTILE_MAXW 16
+#endif
+    const int nks = d->nks;
+    int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
+    const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
+    while (NP > 1 && chunks / NP < 3.0) --NP;
+    const int U = nks * NP;
+    const size_t tshm = cpass_tile_lds(d->PT, R, nks, NP);
+    if (U >= 4 && tshm <= 160 * 1024) {
+      const dim3 tb((unsigned)(64 * std::min(U, QSC_CTILE_MAXW)));
+#define CPASS_TILE_LAUNCH(RPV, ET, KD, LG)                                                     \
+  hipLaunchKernelGGL((cpass_tile_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles), tb, tshm, \
+                     s, (const ET*)c_entries, c_width, c_off, nks, NP, d->PT, lk, E, d->nbins,   \
+                     R, d->K, S, C, w.slab, w.cnll, w.cnsq)
+      QSC_DISPATCH_PASS(CPASS_TILE_LAUNCH);
+#undef CPASS_TILE_LAUNCH
+      QSC_CHECK_LAUNCH();
+      return QSC_OK;
+    }
+  }
   const int xcd_map = (d->ntiles % 8) == 0 ? 1 : 0;
   const dim3 grid((unsigned)((int64_t)d->ntiles * d->nks));
 #define CPASS_LAUNCH(RPV, ET, KD, LG)                                                          \
