@@ -55,7 +55,19 @@ typedef struct qsc_model {
   double sigma;      /* probit noise standard deviation */
   double offset;     /* log-model offset (ignored when log_model == 0) */
   float bounds[QSC_MAX_BOUNDS]; /* bin boundaries as the caller gives them (unclamped) */
+  int32_t loss;      /* QSC_LOSS_PROBIT (0) or QSC_LOSS_SQUARED (1), see below */
+  int32_t reserved_;
 } qsc_model;
+/* loss of the fused passes (qsc_spass / qsc_cpass):
+ *   QSC_LOSS_PROBIT:  -sum_obs log P(y | x)                        qmc/qmc.ipynb :572, :631
+ *   QSC_LOSS_SQUARED:  sum_obs (x - Obs)^2, Obs = (b[y] + b[y+1]) / 2 on the raw edges
+ *                      (get_quantized_obs_from_ordinal, qmc/quantization_model_log.py:43-51):
+ *                      the Euclidean "DowJons" criterion ||Wx (T_hat - Obs)||_F^2 of
+ *                      qmc/qmc_dowjons.ipynb :142, :160 (sigma is unused).
+ * with x = t (linear) or log(t + offset) (log model); the state's nll_* fields then hold the
+ * squared-loss sums. */
+#define QSC_LOSS_PROBIT 0
+#define QSC_LOSS_SQUARED 1
 
 /* Adam hyper-parameters (torch.optim.Adam defaults: betas (0.9, 0.999), eps 1e-8).  The
  * per-step bias corrections are computed on the device from the step counters held in the

@@ -8,6 +8,8 @@ e = (k, p) (Wx = 1; qmc/qmc.ipynb :493, :572):
     P = 0.5 (1 + erf u) - 0.5 (1 + erf w);  nll = -sum log P
     g = (exp(-u^2) - exp(-w^2)) / (a sqrt(pi) P) * (1/(t + offset) if log else 1)
     dS[r,p] = sum_k g C[r,k];  dC[r,k] = sum_p g S[r,p]
+Squared ("DowJons") criterion, qmc/qmc_dowjons.ipynb :142: Obs = (b[y] + b[y+1])/2 (raw edges,
+qmc/quantization_model_log.py:43-51), r = x - Obs, loss = sum r^2, g = 2 r (1/(t + offset) if log).
 """
 import math
 
@@ -43,6 +45,23 @@ def nll_grad(S, C, Y, Wx, b, sigma, offset=0.0, log_model=False):
     dS = C @ g          # (R,K)@(K,P)
     dC = S @ g.T        # (R,P)@(P,K)
     return nll, dS, dC
+
+
+def sq_loss_grad(S, C, Y, Wx, b, offset=0.0, log_model=True):
+    """Squared criterion -> (loss, dS (R,P), dC (R,K)) in fp64."""
+    S = np.asarray(S, np.float64)
+    C = np.asarray(C, np.float64)
+    Y = np.asarray(Y).astype(np.int64)
+    Wx = np.asarray(Wx, np.float64)
+    e = np.asarray(b, dtype=np.float32)
+    obs_val = ((e[Y] + e[Y + 1]) / np.float32(2.0)).astype(np.float64)  # fp32 midpoints
+    T = C.T @ S
+    x = np.log(T + offset) if log_model else T
+    r = x - obs_val
+    obs = Wx != 0
+    loss = float(np.sum(r[obs] ** 2))
+    g = np.where(obs, 2.0 * r * (1.0 / (T + offset) if log_model else 1.0), 0.0)
+    return loss, C @ g, S @ g.T
 
 
 def adam_step(p, m, v, g, step, lr, beta1=0.9, beta2=0.999, eps=1e-8):

@@ -13,6 +13,7 @@ Op-for-op with the reference so that results are bit-identical on the same torch
   mid_bin       qmc/quantization_model_log.py:43-51
   bce_probit    qmc/quantization_model.py:97-113
   masked_nll    qmc/qmc.ipynb :571-572 (log(T_hat + offset), -sum(Wx * log P))
+  dowjons_cost  qmc/qmc_dowjons.ipynb :138-142 (torch.norm(Wx*(log(T_hat+offset)-Obs))**2)
 """
 import numpy as np
 import torch
@@ -86,3 +87,12 @@ def masked_nll(S, C, Y, Wx, b, noise_std, offset=0.0, log_model=False):
     if log_model:
         T_hat = torch.log(T_hat + offset)
     return -torch.sum(Wx * torch.log(prob_probit(Y, T_hat, b, noise_std, log_model)))
+
+
+def dowjons_cost(S, C, Obs, Wx, offset=0.0, log_model=True):
+    """torch.norm(Wx*(T_hat-Obs))**2 with T_hat = log(get_tensor(S, C) + offset)
+    (qmc/qmc_dowjons.ipynb :138-142; Obs = mid_bin(Y, b), :114)."""
+    T_hat = get_tensor(S, C).unsqueeze(1)
+    if log_model:
+        T_hat = torch.log(T_hat + offset)
+    return torch.norm(Wx * (T_hat - Obs)) ** 2

@@ -15,7 +15,18 @@ from . import reference_ops as ro
 
 
 def free_s_solve(S0, C0, Y, Wx, b, sigma, offset=0.0, log_model=False, n_iter=10,
-                 lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2, snapshots=(), timer=None):
+                 lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2, snapshots=(), timer=None,
+                 loss="probit"):
+    """loss="squared": the Euclidean criterion of qmc/qmc_dowjons.ipynb :138-162 in place of
+    the probit likelihood (Obs = mid_bin(Y, b), computed once as at :114)."""
+    if loss == "squared":
+        Obs = ro.mid_bin(Y, b)
+
+        def data_term(S_, C_):
+            return ro.dowjons_cost(S_, C_, Obs, Wx, offset, log_model)
+    else:
+        def data_term(S_, C_):
+            return ro.masked_nll(S_, C_, Y, Wx, b, sigma, offset, log_model)
     S = S0.clone().requires_grad_(True)
     C = C0.clone().requires_grad_(True)
     optC = torch.optim.Adam([C], lr=lr_c)
@@ -25,7 +36,7 @@ def free_s_solve(S0, C0, Y, Wx, b, sigma, offset=0.0, log_model=False, n_iter=10
         t0 = time.perf_counter()
         Sc = S.detach().clone()
         optC.zero_grad()
-        nll = ro.masked_nll(Sc, C, Y, Wx, b, sigma, offset, log_model)
+        nll = data_term(Sc, C)
         cost = nll + lambda_c * torch.norm(C, "fro") + lambda_s * torch.norm(Sc, "fro")
         cost.backward()
         optC.step()
@@ -34,7 +45,7 @@ def free_s_solve(S0, C0, Y, Wx, b, sigma, offset=0.0, log_model=False, n_iter=10
         costs_c.append(cost.item())
         t1 = time.perf_counter()
         optS.zero_grad()
-        nll = ro.masked_nll(S, C, Y, Wx, b, sigma, offset, log_model)
+        nll = data_term(S, C)
         cost = nll + lambda_c * torch.norm(C, "fro") + lambda_s * torch.norm(S, "fro")
         cost.backward()
         optS.step()

@@ -20,13 +20,15 @@ QSC_MAX_R = 16
 QSC_SLICE = 32  # S-format slice (pixel positions per list group), include/qsc.h
 QSC_ENTRY_TAIL = 256  # pad entries after the last list (read-ahead tail), include/qsc.h
 QSC_EINVAL = 100000
+LOSSES = {"probit": 0, "squared": 1}  # QSC_LOSS_PROBIT, QSC_LOSS_SQUARED
 UNOBSERVED = 0xFF
 
 
 class QscModel(ctypes.Structure):
     _fields_ = [("nbounds", ctypes.c_int32), ("log_model", ctypes.c_int32),
                 ("sigma", ctypes.c_double), ("offset", ctypes.c_double),
-                ("bounds", ctypes.c_float * QSC_MAX_BOUNDS)]
+                ("bounds", ctypes.c_float * QSC_MAX_BOUNDS), ("loss", ctypes.c_int32),
+                ("reserved_", ctypes.c_int32)]
 
 
 class QscAdam(ctypes.Structure):
@@ -149,7 +151,7 @@ def stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
-def make_model(bin_boundaries, noise_std, offset=0.0, log_model=False):
+def make_model(bin_boundaries, noise_std, offset=0.0, log_model=False, loss="probit"):
     b = bin_boundaries
     if isinstance(b, torch.Tensor):
         b = b.detach().to("cpu", torch.float32).tolist()
@@ -161,6 +163,9 @@ def make_model(bin_boundaries, noise_std, offset=0.0, log_model=False):
     m.log_model = 1 if log_model else 0
     m.sigma = float(noise_std)
     m.offset = float(offset or 0.0)
+    if loss not in LOSSES:
+        raise ValueError("loss must be one of %s" % sorted(LOSSES))
+    m.loss = LOSSES[loss]
     for i, x in enumerate(b):
         m.bounds[i] = x
     return m

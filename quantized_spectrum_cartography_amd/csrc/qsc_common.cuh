@@ -74,6 +74,15 @@ inline void make_edges(const qsc_model* m, Edges* E) {
   }
 }
 
+// Squared-loss targets: e[c].x = fp32(b[c] + b[c+1]) / 2 on the raw edges, the operation
+// order of get_quantized_obs_from_ordinal (qmc/quantization_model_log.py:48-51).
+inline void make_sq_targets(const qsc_model* m, Edges* E) {
+  for (int c = 0; c < m->nbounds - 1; ++c) {
+    const float lo = m->bounds[c], hi = m->bounds[c + 1];
+    E->e[c] = make_float2((lo + hi) / 2.0f, 0.0f);
+  }
+}
+
 // Correctly rounded x / a for a > 0 (one reciprocal multiply + one FMA residual correction).
 __device__ __forceinline__ float div_a(float x, const Probit& pr) {
   float q = x * pr.inv_a;
@@ -197,9 +206,10 @@ inline Lik make_lik(const qsc_model* m) {
 // Fused-pass likelihood kinds: one active edge (linear one-bit with saturated +-1e5 outer
 // edges: P = F(thr - x) for code 0, 1 - F(thr - x) for code 1, exactly the reference's values),
 // or the general two-edge form (multi-bin and/or log model).
-enum { LIK_ONEBIT = 0, LIK_GENERAL = 1 };
+enum { LIK_ONEBIT = 0, LIK_GENERAL = 1, LIK_SQUARED = 2 };
 
 inline int lik_kind(const qsc_model* m) {
+  if (m->loss == QSC_LOSS_SQUARED) return LIK_SQUARED;
   const Probit p = make_probit(m);
   return (m->log_model == 0 && m->nbounds == 3 && p.lo_sat && p.hi_sat) ? LIK_ONEBIT : LIK_GENERAL;
 }
@@ -212,13 +222,24 @@ __device__ __forceinline__ float div_lik(float x, const Lik& c) {
 
 constexpr float kNegLog2e = -1.44269504088896340736f;
 constexpr float kLn2 = 0.69314718055994530942f;
+constexpr float kInvLn2 = 1.44269504088896340736f;
 
 // One observed entry: t = reconstruction value; returns log2 P (the caller scales the summed
 // NLL by ln 2 once) and g = d(-log P)/dt.  Branch-free; `edges` is only read by the general kind.
 template <int KIND, bool LOG>
 __device__ __forceinline__ void lik_grad(float t, int code, const float2* __restrict__ edges,
                                          const Lik& c, float& log2P, float& g) {
-  if (KIND == LIK_ONEBIT) {
+  if (KIND == LIK_SQUARED) {
+    float x = t, tinv = 1.0f;
+    if (LOG) {
+      const float tp = t + c.offset;
+      x = logf(tp);
+      tinv = __builtin_amdgcn_rcpf(tp);
+    }
+    const float r = x - edges[code].x;
+    g = 2.0f * r * tinv;
+    log2P = -(r * r) * kInvLn2;
+  } else if (KIND == LIK_ONEBIT) {
     const float z = div_lik(c.thr - t, c);
     const float F = 0.5f * (1.0f + erf_fast(z));
     const bool c0 = (code == 0);
@@ -302,7 +323,20 @@ __device__ __forceinline__ f2v log2_2(f2v x) {
 template <int KIND, bool LOG>
 __device__ __forceinline__ void lik_grad2(f2v t, int c0, int c1, const float2* __restrict__ edges,
                                           const Lik& c, f2v& log2P, f2v& g) {
-  if (KIND == LIK_ONEBIT) {
+  if (KIND == LIK_SQUARED) {
+    // r = x - Obs; loss r^2 (returned as -r^2/ln2: the passes scale the summed log2 P by
+    // ln 2); g = d(r^2)/dt = 2 r dx/dt.  t is unscaled for this kind.
+    const float2 e0 = edges[c0], e1 = edges[c1];
+    f2v x = t, tinv = splat2(1.0f);
+    if (LOG) {
+      const f2v tp = t + splat2(c.offset);
+      x = f2v{logf(tp.x), logf(tp.y)};
+      tinv = rcp2(tp);
+    }
+    const f2v r = x - f2v{e0.x, e1.x};
+    g = splat2(2.0f) * r * tinv;
+    log2P = -(r * r) * splat2(kInvLn2);
+  } else if (KIND == LIK_ONEBIT) {
     const f2v z = splat2(c.thr_a) + t;
     const f2v F = splat2(0.5f) * (splat2(1.0f) + erf_fast2(z));
     const f2v Fc = splat2(1.0f) - F;
@@ -396,7 +430,18 @@ template <int KIND, bool LOG>
 __device__ __forceinline__ void lik_grad4(f4v t, const int (&cd)[4],
                                           const float2* __restrict__ edges, const Lik& c,
                                           f4v& log2P, f4v& g) {
-  if (KIND == LIK_ONEBIT) {
+  if (KIND == LIK_SQUARED) {
+    const float2 e0 = edges[cd[0]], e1 = edges[cd[1]], e2 = edges[cd[2]], e3 = edges[cd[3]];
+    f4v x = t, tinv = splat4(1.0f);
+    if (LOG) {
+      const f4v tp = t + splat4(c.offset);
+      x = f4v{logf(tp.x), logf(tp.y), logf(tp.z), logf(tp.w)};
+      tinv = rcp4(tp);
+    }
+    const f4v r = x - f4v{e0.x, e1.x, e2.x, e3.x};
+    g = splat4(2.0f) * r * tinv;
+    log2P = -(r * r) * splat4(kInvLn2);
+  } else if (KIND == LIK_ONEBIT) {
     const f4v z = splat4(c.thr_a) + t;
     const f4v F = splat4(0.5f) * (splat4(1.0f) + erf_fast4(z));
     const f4v Fc = splat4(1.0f) - F;

@@ -443,7 +443,7 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
   constexpr int CP = Pitch<RP>::v;
   constexpr int RH = RP / 2;  // row elements updated per lane (half row)
   // linear models evaluate the entries in the scaled form t' = -t/a (lik_grad2)
-  const float own_scale = LOG ? 1.0f : -lk.inv_a;
+  const float own_scale = (LOG || KIND == LIK_SQUARED) ? 1.0f : -lk.inv_a;
   // all LDS carved from the 16-B aligned dynamic region (no statics ahead of it)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   Scalars& sc = *reinterpret_cast<Scalars*>(smem);            // 32 B reserved
@@ -671,7 +671,7 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   STAMP(wg, 1);
 
   // 3. likelihood + gradient over the part lists
-  const float own_scale = LOG ? 1.0f : -lk.inv_a;  // scaled form t' = -t/a (lik_grad2)
+  const float own_scale = (LOG || KIND == LIK_SQUARED) ? 1.0f : -lk.inv_a;  // scaled form t' = -t/a (lik_grad2)
   f2v own[RP / 2];
 #pragma unroll
   for (int j = 0; j < RP / 2; ++j)
@@ -750,7 +750,7 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
   const int t = blockIdx.x;
   const int Kp = nks * 64;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const float own_scale = LOG ? 1.0f : -lk.inv_a;  // scaled form t' = -t/a (lik_grad2)
+  const float own_scale = (LOG || KIND == LIK_SQUARED) ? 1.0f : -lk.inv_a;  // scaled form t' = -t/a (lik_grad2)
   [[maybe_unused]] const int wg = blockIdx.x * (kCTBlock / 64) + w;  // (diagnostic stamps)
   STAMP(wg, 0);
   RSTAMP(wg, 28);
@@ -1181,39 +1181,25 @@ size_t cpass_lds(const qsc_obs_desc* d, int R) {
 #define STREAM(s) reinterpret_cast<hipStream_t>(s)
 
 // dispatch over (RP, entry type, likelihood kind, log) for a kernel template K<RP,E,KIND,LOG,...>
+#define QSC_DISPATCH_RP(LAUNCH, KD, LG)                                                  \
+  do {                                                                                   \
+    if (d->wide) {                                                                       \
+      if (RP == 4) LAUNCH(4, uint32_t, KD, LG);                                          \
+      else if (RP == 8) LAUNCH(8, uint32_t, KD, LG);                                     \
+      else LAUNCH(16, uint32_t, KD, LG);                                                 \
+    } else {                                                                             \
+      if (RP == 4) LAUNCH(4, uint16_t, KD, LG);                                          \
+      else if (RP == 8) LAUNCH(8, uint16_t, KD, LG);                                     \
+      else LAUNCH(16, uint16_t, KD, LG);                                                 \
+    }                                                                                    \
+  } while (0)
 #define QSC_DISPATCH_PASS(LAUNCH)                                                        \
   do {                                                                                   \
-    if (kind == LIK_ONEBIT) {                                                            \
-      if (d->wide) {                                                                     \
-        if (RP == 4) LAUNCH(4, uint32_t, LIK_ONEBIT, false);                             \
-        else if (RP == 8) LAUNCH(8, uint32_t, LIK_ONEBIT, false);                        \
-        else LAUNCH(16, uint32_t, LIK_ONEBIT, false);                                    \
-      } else {                                                                           \
-        if (RP == 4) LAUNCH(4, uint16_t, LIK_ONEBIT, false);                             \
-        else if (RP == 8) LAUNCH(8, uint16_t, LIK_ONEBIT, false);                        \
-        else LAUNCH(16, uint16_t, LIK_ONEBIT, false);                                    \
-      }                                                                                  \
-    } else if (m->log_model) {                                                           \
-      if (d->wide) {                                                                     \
-        if (RP == 4) LAUNCH(4, uint32_t, LIK_GENERAL, true);                             \
-        else if (RP == 8) LAUNCH(8, uint32_t, LIK_GENERAL, true);                        \
-        else LAUNCH(16, uint32_t, LIK_GENERAL, true);                                    \
-      } else {                                                                           \
-        if (RP == 4) LAUNCH(4, uint16_t, LIK_GENERAL, true);                             \
-        else if (RP == 8) LAUNCH(8, uint16_t, LIK_GENERAL, true);                        \
-        else LAUNCH(16, uint16_t, LIK_GENERAL, true);                                    \
-      }                                                                                  \
-    } else {                                                                             \
-      if (d->wide) {                                                                     \
-        if (RP == 4) LAUNCH(4, uint32_t, LIK_GENERAL, false);                            \
-        else if (RP == 8) LAUNCH(8, uint32_t, LIK_GENERAL, false);                       \
-        else LAUNCH(16, uint32_t, LIK_GENERAL, false);                                   \
-      } else {                                                                           \
-        if (RP == 4) LAUNCH(4, uint16_t, LIK_GENERAL, false);                            \
-        else if (RP == 8) LAUNCH(8, uint16_t, LIK_GENERAL, false);                       \
-        else LAUNCH(16, uint16_t, LIK_GENERAL, false);                                   \
-      }                                                                                  \
-    }                                                                                    \
+    if (kind == LIK_ONEBIT) QSC_DISPATCH_RP(LAUNCH, LIK_ONEBIT, false);                  \
+    else if (kind == LIK_SQUARED && m->log_model) QSC_DISPATCH_RP(LAUNCH, LIK_SQUARED, true); \
+    else if (kind == LIK_SQUARED) QSC_DISPATCH_RP(LAUNCH, LIK_SQUARED, false);           \
+    else if (m->log_model) QSC_DISPATCH_RP(LAUNCH, LIK_GENERAL, true);                   \
+    else QSC_DISPATCH_RP(LAUNCH, LIK_GENERAL, false);                                    \
   } while (0)
 
 extern "C" {
@@ -1261,7 +1247,10 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
   make_edges(m, &E);
   const Lik lk = make_lik(m);
   const int kind = lik_kind(m);
-  if (!m->log_model) scale_edges(&E, m->nbounds - 1, lk.a);
+  if (kind == LIK_SQUARED)
+    make_sq_targets(m, &E);
+  else if (!m->log_model)
+    scale_edges(&E, m->nbounds - 1, lk.a);
   const int nslices = d->Pp / QSC_SLICE;
   const int bpc = RP > 8 ? 2 : RP == 8 ? QSC_SPASS_BPC8 : QSC_SPASS_BPC;
   const dim3 grid((unsigned)std::min<int64_t>(ceil_div(nslices, kSWaves), (int64_t)cu_count() * bpc));
@@ -1302,7 +1291,10 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
   make_edges(m, &E);
   const Lik lk = make_lik(m);
   const int kind = lik_kind(m);
-  if (!m->log_model) scale_edges(&E, m->nbounds - 1, lk.a);
+  if (kind == LIK_SQUARED)
+    make_sq_targets(m, &E);
+  else if (!m->log_model)
+    scale_edges(&E, m->nbounds - 1, lk.a);
   hipStream_t s = STREAM(stream);
 #ifndef QSC_CPASS_TILE
 #define QSC_CPASS_TILE 1

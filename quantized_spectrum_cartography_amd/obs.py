@@ -36,10 +36,12 @@ class Observations:
       bin_boundaries, noise_std, offset, log_model: the probit model (see quantization_model*).
       perm: optional (Pp,) int32 pixel order shared across ranks (K-slab sharding).
       tile: optional C-pass tile size (positions, multiple of 64).
+      loss: "probit" (the likelihood of qmc/qmc.ipynb) or "squared" (the Euclidean criterion
+            ||Wx (T_hat - Obs)||^2 of qmc/qmc_dowjons.ipynb :142, Obs the bin midpoints).
     """
 
     def __init__(self, Y, Wx, bin_boundaries, noise_std, offset=0.0, log_model=False, perm=None,
-                 tile=None, R_hint=8, count_hook=None):
+                 tile=None, R_hint=8, count_hook=None, loss="probit"):
         K = Y.shape[0]
         I, J = Y.shape[-2], Y.shape[-1]
         P = I * J
@@ -49,7 +51,8 @@ class Observations:
             raise ValueError("tile must be a positive multiple of 64")
         self.Pp = -(-P // PT) * PT  # whole tiles; padding positions carry no observations
         self.model = _lib.make_model(bin_boundaries, noise_std, offset if log_model else 0.0,
-                                     log_model)
+                                     log_model, loss=loss)
+        self.loss = loss
         self.log_model = bool(log_model)
         self.noise_std = float(noise_std)
         self.offset = float(offset or 0.0)

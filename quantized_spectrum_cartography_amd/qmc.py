@@ -126,13 +126,16 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
           log_model=False, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2, max_iter=500,
           betas=(0.9, 0.999), eps=1e-8, project_c=True, generator=None, Z_init=None,
           restart=False, restart_samples=(200, 200), T_true=None, nmse_every=0,
-          use_graph=False, obs=None, tile=None, callback=None):
+          use_graph=False, obs=None, tile=None, callback=None, loss="probit"):
     """Alternating S/C probit-MLE (qmc/qmc.ipynb :559-645).
 
     Args mirror the notebook globals: Y (K,1,I,J) bin indices, Wx (K,1,I,J) 0/1 mask,
     bin_boundaries / noise_std / offset of the model, lambda_c = lambda_s = 100,
     lr_c = 5e-3, lr_s = 1e-2, max_iter = 500.  With `generator` the S-step optimises Z_init
     through S = generator(Z) (Adam on Z, the network frozen); otherwise S is free.
+    loss="squared" replaces the probit likelihood by the Euclidean criterion
+    ||Wx (T_hat - Obs)||_F^2 of qmc/qmc_dowjons.ipynb :142-162 (Obs = bin midpoints,
+    get_quantized_obs_from_ordinal); the cost history then holds that criterion.
     Returns a SolveResult with S (R,1,I,J) and C (R,K) on the GPU.
     """
     K = Y.shape[0]
@@ -142,7 +145,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
              (C_init.shape[0] if C_init is not None else Z_init.shape[0]))
     if obs is None:
         obs = Observations(Y, Wx, bin_boundaries, noise_std, offset=offset or 0.0,
-                           log_model=log_model, tile=tile, R_hint=R)
+                           log_model=log_model, tile=tile, R_hint=R, loss=loss)
     if C_init is None:
         C_init = torch.zeros(R, K)
     if generator is None:

@@ -223,3 +223,48 @@ def test_dip_solver_256():
     res = dip.solve(Y, Wx, b, 5.0, R, offset=1e-10, max_iter=4)
     assert res.S.shape == (R, 1, N, N)
     assert np.all(np.isfinite(res.costs_c))
+
+
+@pytest.mark.parametrize("seed,R,I,J,K,log_model,tile", [
+    (31, 4, 32, 32, 16, True, None),     # log model (qmc_dowjons.ipynb form)
+    (32, 8, 64, 64, 128, True, 512),     # rank 8, two k-slices
+    (33, 3, 40, 40, 70, False, None),    # linear model, ragged k
+])
+def test_squared_pass_vs_explicit(seed, R, I, J, K, log_model, tile):
+    """Fused squared-criterion pass (QSC_LOSS_SQUARED) vs the fp64 closed form, 1e-5."""
+    from quantized_spectrum_cartography_amd import fused
+    from quantized_spectrum_cartography_amd.obs import Observations
+    d = _random_case(seed, R, I, J, K, 0.2, 4, log_model)
+    obs = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], offset=d["offset"],
+                       log_model=log_model, R_hint=R, tile=tile, loss="squared")
+    S = d["S0"].cuda().requires_grad_(True)
+    C = d["C0"].cuda().requires_grad_(True)
+    loss = fused.ProbitNLL.apply(S, C, obs)
+    loss.backward()
+    P = I * J
+    rl, rdS, rdC = explicit.sq_loss_grad(d["S0"].reshape(R, P).numpy(), d["C0"].numpy(),
+                                         d["Y"].reshape(K, P).numpy(), d["Wx"].reshape(K, P).numpy(),
+                                         d["b"].numpy(), d["offset"], log_model)
+    assert abs(loss.item() - rl) / abs(rl) < 1e-5
+    assert rel_fro(S.grad.cpu().reshape(R, P).numpy(), rdS) < 1e-5
+    assert rel_fro(C.grad.cpu().numpy(), rdC) < 1e-5
+
+
+def test_squared_solver_vs_reference_golden(golden):
+    """Free-S solver with loss="squared" (qmc/qmc_dowjons.ipynb :114-162) vs the reference."""
+    from quantized_spectrum_cartography_amd import qmc
+    g = golden("solve_sq_32")
+    n = int(g["n_iter"])
+    kw = dict(offset=float(g["offset"]), log_model=True, lambda_c=float(g["lam_c"]),
+              lambda_s=float(g["lam_s"]), lr_c=float(g["lr_c"]), lr_s=float(g["lr_s"]),
+              loss="squared")
+    args = (T(g["Y"].astype(np.int64)), T(g["Wx"].astype(np.float32)), T(g["b"]),
+            float(g["sigma"]))
+    r1 = qmc.solve(*args, S_init=T(g["S0"]), C_init=T(g["C0"]), max_iter=1, **kw)
+    assert rel_fro(r1.S.cpu().numpy(), g["S_it1"]) < 1e-5
+    assert rel_fro(r1.C.cpu().numpy(), g["C_it1"]) < 1e-5
+    rn = qmc.solve(*args, S_init=T(g["S0"]), C_init=T(g["C0"]), max_iter=n, **kw)
+    assert rel_fro(rn.S.cpu().numpy(), g["S_it%d" % n]) < 1e-5
+    assert rel_fro(rn.C.cpu().numpy(), g["C_it%d" % n]) < 1e-5
+    assert np.allclose(rn.costs_c, g["costs_c"], rtol=1e-5)
+    assert np.allclose(rn.costs_s, g["costs_s"], rtol=1e-5)

@@ -17,7 +17,10 @@ The solver goldens re-enact the alternating C-step / S-step of qmc/qmc.ipynb cel
 (the free-S form of backup/notebooks/onebit_lowrank.ipynb:1230-1236), using the
 reference's get_tensor / prob_probit and torch.optim.Adam verbatim.
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/make_golden.py
+The "DowJons" squared-criterion golden (solve_sq_32) re-enacts qmc/qmc_dowjons.ipynb :114-162
+the same way (free S), with the reference's get_quantized_obs_from_ordinal / get_tensor.
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/make_golden.py [solve_sq_32]
 """
 import io
 import os
@@ -233,6 +236,48 @@ def gen_solve(name, d, log_model, n_iter, lam_c=100.0, lam_s=100.0, lr_c=5e-3, l
 
 
 # ----------------------------------------------------------------------------------
+# Euclidean ("DowJons") criterion: qmc/qmc_dowjons.ipynb :114-162 with S as the free Adam
+# variable: Obs = get_quantized_obs_from_ordinal(Y, b, std) once, then per C- and S-step
+#   cost = torch.norm(Wx*(log(get_tensor(S, C)+offset) - Obs))**2 + lam_c||C|| + lam_s||S||
+# ----------------------------------------------------------------------------------
+def gen_solve_sq(name, d, n_iter, lam_c=100.0, lam_s=100.0, lr_c=5e-3, lr_s=1e-2):
+    Obs = qml.get_quantized_obs_from_ordinal(d["Y"], d["b"], d["sigma"])
+    S = d["S0"].clone().requires_grad_(True)
+    C = d["C0"].clone().requires_grad_(True)
+    optC = torch.optim.Adam([C], lr=lr_c)
+    optS = torch.optim.Adam([S], lr=lr_s)
+    costs_c, costs_s, snaps = [], [], {}
+    for i in range(n_iter):
+        Sc = S.detach().clone()
+        optC.zero_grad()
+        T_hat = torch.log(qml.get_tensor(Sc, C).unsqueeze(1) + d["offset"])
+        cost = (torch.norm(d["Wx"] * (T_hat - Obs)) ** 2 + lam_c * torch.norm(C, "fro")
+                + lam_s * torch.norm(Sc, "fro"))
+        cost.backward()
+        optC.step()
+        with torch.no_grad():
+            C[C < 0] = 0
+        costs_c.append(cost.item())
+        optS.zero_grad()
+        T_hat = torch.log(qml.get_tensor(S, C).unsqueeze(1) + d["offset"])
+        cost = (torch.norm(d["Wx"] * (T_hat - Obs)) ** 2 + lam_c * torch.norm(C, "fro")
+                + lam_s * torch.norm(S, "fro"))
+        cost.backward()
+        optS.step()
+        costs_s.append(cost.item())
+        if i + 1 in (1, n_iter):
+            snaps["S_it%d" % (i + 1)] = f32(S)
+            snaps["C_it%d" % (i + 1)] = f32(C)
+    out = dict(S0=f32(d["S0"]), C0=f32(d["C0"]), Y=d["Y"].numpy().astype(np.uint8),
+               Wx=f32(d["Wx"]).astype(np.uint8), b=f32(d["b"]), sigma=np.float32(d["sigma"]),
+               offset=np.float64(d["offset"]), log_model=np.int32(1), lam_c=np.float32(lam_c),
+               lam_s=np.float32(lam_s), lr_c=np.float32(lr_c), lr_s=np.float32(lr_s),
+               n_iter=np.int32(n_iter), Obs=f32(Obs), costs_c=np.array(costs_c),
+               costs_s=np.array(costs_s), **snaps)
+    save(name, **out)
+
+
+# ----------------------------------------------------------------------------------
 # shipped fixture (config 1) and nlls known answers
 # ----------------------------------------------------------------------------------
 def gen_mat():
@@ -264,12 +309,16 @@ def gen_nlls():
 
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if sys.argv[1:] == ["solve_sq_32"]:  # add only this fixture
+        gen_solve_sq("solve_sq_32", synth_log(20267, 3, 32, 32, 16), n_iter=10)
+        return
     gen_ops()
     gen_pass("pass_onebit_small", synth_onebit(20260, 3, 16, 16, 12), log_model=False)
     gen_pass("pass_onebit_64", synth_onebit(20261, 4, 64, 64, 32), log_model=False)
     gen_pass("pass_log_small", synth_log(20265, 3, 16, 16, 12), log_model=True)
     gen_solve("solve_onebit_64", synth_onebit(20262, 4, 64, 64, 32), log_model=False, n_iter=10)
     gen_solve("solve_log_32", synth_log(20266, 3, 32, 32, 16), log_model=True, n_iter=10)
+    gen_solve_sq("solve_sq_32", synth_log(20267, 3, 32, 32, 16), n_iter=10)
     gen_mat()
     gen_nlls()
 
