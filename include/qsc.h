@@ -314,6 +314,33 @@ QSC_API int qsc_gram_rhs(const float* S, const float* T, const float* w, int32_t
 QSC_API int qsc_chol_solve(const float* G, const float* B, int32_t R, int32_t K, float lambda,
                            float* X, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * SPA warm start and non-negative C-update.
+ *   qsc_syrk:  G[K][K] = sum_p w[p] T[a,p] T[b,p]   (T row-major [K][P]; K x K Gram of the
+ *              data on the f32 MFMA; deterministic)
+ *   qsc_spa:   backup/algorithms/NMF_SPA.m:1-29 on Tm = T' restricted to the pixel mask w
+ *              (w[p] != 0 marks an observed pixel, NULL = all): SPA (NMF_SPA.m:31-56) picks up
+ *              to R frequency bins into sel[R] (-1 padded; *count = how many), then
+ *              C[R][K] = rows of (inv(Sm'Sm) Sm' Tm)' after ColumnPositive, C >= 0 and
+ *              unit-norm (ColumnNormalization), S[R][P] = mask * T[sel] * d (Sm' of the
+ *              reference, d = the column norms removed from C).  Optional G_out[K][K] copy.
+ *              K <= 4096.  Stream-ordered: *count is device memory.
+ *   qsc_nnls:  backup/algorithms/joint_opt_ae.m:409-417 lsqnonneg([Q'; lambda I], [y; 0]) per
+ *              bin in normal-equation form: X[:,k] = argmin_{x >= 0} ||A x - b_k||, given
+ *              G = Q Q^T (R x R) and B = Q Y^T (R x K); `lambda` is added to the diagonal of G
+ *              (pass the reference's lambda squared).  Lawson-Hanson active set, one thread per
+ *              bin; NaN column if a passive sub-system is not positive definite.
+ * ------------------------------------------------------------------------------------- */
+QSC_API size_t qsc_syrk_workspace_bytes(int32_t K, int32_t P);
+QSC_API int qsc_syrk(const float* T, const float* w, int32_t K, int32_t P, float* G, void* ws,
+                     size_t ws_bytes, void* stream);
+QSC_API size_t qsc_spa_workspace_bytes(int32_t K, int32_t P, int32_t R);
+QSC_API int qsc_spa(const float* T, const float* w, int32_t K, int32_t P, int32_t R,
+                    int32_t* sel, int32_t* count, float* C, float* S, float* G_out, void* ws,
+                    size_t ws_bytes, void* stream);
+QSC_API int qsc_nnls(const float* G, const float* B, int32_t R, int32_t K, float lambda,
+                     float* X, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,3 +54,24 @@ def chol_solve(G, B, lam=0.0):
 def ls_spectra(S, T, w=None, lam=0.0):
     """Least-squares power spectra C (R, K) for fixed S: argmin ||T - C^T S||^2 + lam ||C||^2."""
     return chol_solve(gram(S, w), cross(S, T, w), lam)
+
+
+def nnls(G, B, lam=0.0):
+    """X (R, K) with X[:, k] = argmin_{x >= 0} x^T (G + lam I) x / 2 - B[:, k]^T x (HIP)."""
+    R, K = B.shape
+    Gd = _dev(G.to(torch.float32))
+    Bd = _dev(B.to(torch.float32))
+    X = torch.empty_like(Bd)
+    _lib.call("qsc_nnls", _lib.ptr(Gd), _lib.ptr(Bd), R, K, float(lam), _lib.ptr(X),
+              _lib.stream())
+    return X
+
+
+def nnls_spectra(Q, Y, lam=0.0, w=None):
+    """Non-negative C-update of backup/algorithms/joint_opt_ae.m:404-417.
+
+    Q (R, P): spatial factors at the sampled pixels (Sm*W); Y (K, P): the data there (Tm*W).
+    For every bin k, c_k = lsqnonneg([Q'; lam I], [Y(k,:)'; 0]); returns C (R, K) (the
+    reference stacks the c_k' as rows of a K x R matrix).  Normal equations on the MFMA Gram,
+    Lawson-Hanson active set per bin on the GPU."""
+    return nnls(gram(Q, w), cross(Q, Y, w), float(lam) ** 2)
