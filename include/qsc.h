@@ -341,6 +341,19 @@ QSC_API int qsc_spa(const float* T, const float* w, int32_t K, int32_t P, int32_
 QSC_API int qsc_nnls(const float* G, const float* B, int32_t R, int32_t K, float lambda,
                      float* X, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Synthetic radio maps: qmc/generate_map.m:80-113.
+ *   S[r][i*J+j] = min(1, (d/d0)^-alpha[r]) * 10^(shadow[r][i*J+j]/10), d = |(j res, i res) -
+ *   (loc[2r], loc[2r+1])|, then S[r] /= ||S[r]||_F (f64, fixed order; norms[r] = the norm if
+ *   non-NULL) and, if db, S = 10 log10(S).  shadow: the correlated shadowing field in dB
+ *   (Shadowing_data.m; drawn by circulant embedding in maps.py).  The map is then
+ *   qsc_reconstruct(S, C).
+ * ------------------------------------------------------------------------------------- */
+QSC_API size_t qsc_map_compose_workspace_bytes(int32_t R, int32_t I, int32_t J);
+QSC_API int qsc_map_compose(const float* shadow, const float* loc, const float* alpha, int32_t R,
+                            int32_t I, int32_t J, float res, float d0, int32_t db, float* S,
+                            float* norms, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

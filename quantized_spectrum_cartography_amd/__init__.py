@@ -12,9 +12,13 @@ dip.py entry points.  Module map (reference file in parentheses):
   qmc                     (qmc/qmc.ipynb, qmc/qmc.py)      alternating solver
   dip                     (qmc/dip.py, empty upstream)     deep-image-prior solver
   obs, fused                                               packed observations, fused passes
-  gram                    (backup/algorithms/NMF_SPA.m)    R x R normal equations (MFMA)
+  gram                    (backup/algorithms/NMF_SPA.m)    R x R normal equations (MFMA),
+                          (joint_opt_ae.m:404-417)         non-negative C-update (NNLS)
+  spa                     (backup/algorithms/NMF_SPA.m)    SPA warm start (MFMA K x K Gram)
+  maps                    (qmc/generate_map.m,             scalable synthetic radio maps
+                           qmc/Shadowing_data.m)
   metrics, synthetic                                       SLF/map NMSE, benchmark inputs
-  distributed                                              K-slab sharding over RCCL
+  distributed                                              IJ-/K-slab sharding over RCCL
 
 All arithmetic on the path runs in libqsc_hip.so (HIP, gfx950); there is no CPU fallback.
 """

@@ -13,7 +13,8 @@ import tempfile
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libqsc_hip.so")
-SOURCES = ["qsc_ops.hip", "qsc_obs.hip", "qsc_pass.hip", "qsc_gram.hip", "qsc_spa.hip"]
+SOURCES = ["qsc_ops.hip", "qsc_obs.hip", "qsc_pass.hip", "qsc_gram.hip", "qsc_spa.hip",
+           "qsc_map.hip"]
 ARCH = os.environ.get("QSC_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: hipcc contracts a*b+c into FMA by default, which would change the
 # reference's separately rounded products and sums (get_tensor, quantize); FMAs that are
