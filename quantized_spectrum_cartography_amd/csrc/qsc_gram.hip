@@ -77,16 +77,26 @@ __global__ void __launch_bounds__(kGBlock) gram_kernel(const float* __restrict__
   }
 }
 
-// out[i][jb + j] for i < R, jb + j < nb_rows: sum of partials over blocks, fixed order
+// out[i][jb + j] for i < R, jb + j < nb_rows: sum of partials over blocks in a fixed order.
+// Grid (nby, 4): a workgroup owns 64 of the 256 tile elements; its 4 waves take interleaved
+// quarters of the blocks (memory-level parallelism), combined in a fixed order through LDS.
 __global__ void __launch_bounds__(256) gram_reduce_kernel(const float* __restrict__ partial,
                                                           int nblk, int R, int nb_rows,
                                                           float* __restrict__ out) {
-  const int e = threadIdx.x;  // 16x16 element
-  const int i = e >> 4, j = e & 15;
+  __shared__ float sh[4][64];
+  const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int e = blockIdx.y * 64 + l;  // 16x16 element
   const int jb = blockIdx.x * 16;
+  const float* src = partial + (int64_t)blockIdx.x * nblk * 256 + e;
   float s = 0.0f;
-  for (int b = 0; b < nblk; ++b) s += partial[((int64_t)blockIdx.x * nblk + b) * 256 + e];
-  if (i < R && jb + j < nb_rows) out[(int64_t)i * nb_rows + jb + j] = s;
+  for (int b = q; b < nblk; b += 4) s += src[(int64_t)b * 256];
+  sh[q][l] = s;
+  __syncthreads();
+  if (q == 0) {
+    const float t = ((sh[0][l] + sh[1][l]) + sh[2][l]) + sh[3][l];
+    const int i = e >> 4, j = e & 15;
+    if (i < R && jb + j < nb_rows) out[(int64_t)i * nb_rows + jb + j] = t;
+  }
 }
 
 // X[R][K] = (G + lambda I)^-1 B, Cholesky in double, one workgroup
@@ -149,7 +159,7 @@ QSC_API int qsc_gram(const float* S, const float* w, int32_t R, int32_t P, float
   hipLaunchKernelGGL(gram_kernel, dim3(kGBlocks, 1), dim3(kGBlock), 0, STREAM(stream), S, S, w, R,
                      P, R, (int64_t)P, aligned, (float*)ws);
   QSC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3(1), dim3(256), 0, STREAM(stream), (const float*)ws,
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3(1, 4), dim3(256), 0, STREAM(stream), (const float*)ws,
                      kGBlocks, R, R, G);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
@@ -165,7 +175,7 @@ QSC_API int qsc_gram_rhs(const float* S, const float* T, const float* w, int32_t
   hipLaunchKernelGGL(gram_kernel, dim3(kGBlocks, nby), dim3(kGBlock), 0, STREAM(stream), S, T, w,
                      R, P, K, (int64_t)P, aligned, (float*)ws);
   QSC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3(nby), dim3(256), 0, STREAM(stream),
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3(nby, 4), dim3(256), 0, STREAM(stream),
                      (const float*)ws, kGBlocks, R, K, B);
   QSC_CHECK_LAUNCH();
   return QSC_OK;

@@ -48,6 +48,16 @@ def main():
     Q = Sg
     Gq, Bq = gram.gram(Q), gram.cross(Q, Tt)
     t_nnls = timed(lambda: gram.nnls(Gq, Bq, 0.25))
+    # map compose (qsc_map_compose): R = 16 fields of 1024 x 1024, HBM-bound
+    from quantized_spectrum_cartography_amd import maps
+    Rm, Im, Jm = 16, 1024, 1024
+    sh = torch.randn((Rm, Im, Jm), device="cuda")
+    loc = np.stack([1023 * np.random.default_rng(0).random(Rm), 1023 * np.random.default_rng(1).random(Rm)], 1)
+    al = 2 + 0.5 * np.random.default_rng(2).random(Rm)
+    ld = torch.as_tensor(loc, dtype=torch.float32, device="cuda")
+    ad = torch.as_tensor(al, dtype=torch.float32, device="cuda")
+    t_map = timed(lambda: maps.compose(sh, ld, ad))
+    map_bytes = Rm * Im * Jm * 4 * 4  # read shadow, write S, re-read + write in the normalisation
     t0 = time.perf_counter()
     Co, So, idx_o = ospa.nmf_spa(T, R)
     t_cpu = time.perf_counter() - t0
@@ -57,6 +67,8 @@ def main():
         "syrk_f32_frac_of_157.3TF": flops / t_syrk / 1e6 / 157.3,
         "spa_total_us": t_spa, "spa_gram_f64_TFLOPs_upper_bound": flops / t_spa / 1e6,
         "nnls_us": t_nnls,
+        "map_compose_us": t_map, "map_compose_GBs": map_bytes / t_map / 1e3,
+        "map_compose_frac_of_8TBs": map_bytes / t_map / 1e3 / 8000.0,
         "picked_bins_match_oracle": idx == idx_o,
         "cpu_oracle_nmf_spa_s": t_cpu, "cpu_threads": torch.get_num_threads(),
     }
