@@ -266,6 +266,17 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
 QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_t* c_width,
                       const int64_t* c_off, const qsc_model* m, int32_t R, const float* S,
                       const float* C, void* ws, size_t ws_bytes, void* stream);
+/* Fused S-step + next C-pass (free-S solver, Adam on S): one launch equal to qsc_spass(mode 1)
+ * followed by qsc_cpass at the updated S -- same partials, same state protocol -- so a solver
+ * runs  cpass, cfinish, (scpass, cfinish) x (n-1), spass  for n outer iterations
+ * (qmc/qmc.ipynb :562-634).  One workgroup per C-pass pixel tile: the tile's S-step results
+ * feed its C-pass through LDS.  Available when qsc_scpass_supported(d, R) (R <= 8). */
+QSC_API int qsc_scpass_supported(const qsc_obs_desc* d, int32_t R);
+QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
+                       const int64_t* s_off, const void* c_entries, const int32_t* c_width,
+                       const int64_t* c_off, const qsc_model* m, int32_t R, float* S,
+                       const float* C, float* mS, float* vS, const qsc_adam* adam,
+                       float lambda_s, qsc_state* st, void* ws, size_t ws_bytes, void* stream);
 /* reduce the C-pass slab (fixed order).  mode 0: write dC (NLL gradient only); mode 1: fused
  * C-step: dC + lambda_c*C/||C||, Adam on C, projection; mode 2 (IJ-slab sharding): as mode 0 and
  * dC[R*K] (dC holds R*K + 1 floats) receives this shard's ||S||^2 after the S-pass partials are

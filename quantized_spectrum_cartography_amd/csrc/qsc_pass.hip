@@ -862,6 +862,213 @@ size_t cpass_tile_lds(int PT, int R, int nks, int NP) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Fused S-step + next C-pass, one workgroup per C-pass pixel tile (RP <= 8, 16 waves).
+// The tile's whole position slices (tile_pos) get their S-step first -- likelihood, dS and
+// Adam exactly as spass_kernel, wave w taking the tile's slices w, 2*16-1-w, ... (snake over
+// the count-sorted slices) -- and the new S rows are written to HBM (S, mS, vS) AND into the
+// LDS tile; after one barrier the same workgroup runs the tile's C-pass units exactly as
+// cpass_tile_kernel, at the new S, for the NEXT iteration's C-step.  So one launch replaces
+// spass + cpass: no kernel boundary between them and no re-read / staging of the S tile (the
+// C-pass of iteration i+1 reads only S_i of its own tile, and C_i, which the S-step also used).
+// Kernel sequence semantics are unchanged: spass_i then cpass_{i+1} (same partials, same
+// state protocol), so a solver runs cpass+cfinish, then (fused + cfinish) x (n-1), then spass.
+// ---------------------------------------------------------------------------------------
+template <int RP, typename E, int KIND, bool LOG>
+__global__ void __launch_bounds__(kCTBlock) scfused_kernel(
+    const E* __restrict__ s_ent, const int* __restrict__ s_width, const int64_t* __restrict__ s_off,
+    const E* __restrict__ c_ent, const int* __restrict__ c_width, const int64_t* __restrict__ c_off,
+    int nks, int NP, int PT, Lik lk, Edges E_, int nbins, int R, int K, float* __restrict__ S,
+    const float* __restrict__ C, float* __restrict__ mS, float* __restrict__ vS, qsc_adam ad,
+    float lambda_s, qsc_state* __restrict__ st, float* __restrict__ part_nll_s,
+    float* __restrict__ part_nsq_s, float* __restrict__ slab, float* __restrict__ part_nll_c,
+    float* __restrict__ cnsq) {
+  using V4 = typename Ent<E>::V4;
+  constexpr int CP = Pitch<RP>::v;  // C^T row pitch == S tile row pitch
+  constexpr int RH = RP / 2;
+  constexpr bool ADAM = true;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  Scalars& sc = *reinterpret_cast<Scalars*>(smem);                // 32 B
+  float* Cl = smem + 8;                                            // [K][CP]
+  float2* El = reinterpret_cast<float2*>(Cl + (size_t)K * CP);      // [256]
+  float* Sl = reinterpret_cast<float*>(El + 256);                   // [PT][CP]
+  float* Pl = Sl + (size_t)PT * CP;                                 // [U][R][64]  (NP > 1)
+  const int NW = blockDim.x >> 6;
+  const int U = nks * NP;
+  float* Nl = Pl + (NP > 1 ? (size_t)U * R * 64 : 0);               // [max(U,16)]
+  const int t = blockIdx.x, nt = gridDim.x;
+  const int Kp = nks * 64;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int p = lane & (QSC_SLICE - 1), h = lane >> 5;
+  const uint32_t hmask = 0u - (uint32_t)h;
+  const float own_scale = (LOG || KIND == LIK_SQUARED) ? 1.0f : -lk.inv_a;
+  const int nsl = PT / QSC_SLICE;  // slices per tile
+  // this wave's n-th slice of the tile (local index) and its global slice
+  auto local_of = [&](int n) { return n * NW + ((n & 1) ? (NW - 1 - w) : w); };
+  auto global_of = [&](int i) { return i * nt + ((i & 1) ? (nt - 1 - t) : t); };
+
+  // 1. first slice's reads, then C^T + edges into LDS
+  int il = local_of(0);
+  SliceIn<RP, E, ADAM> cur;
+  slice_load(cur, s_ent, s_width, s_off, global_of(il < nsl ? il : 0), p, h, S, mS, vS);
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    float v[RP];
+#pragma unroll
+    for (int r = 0; r < RP; ++r) v[r] = (r < R) ? C[(int64_t)r * K + k] : 0.0f;
+#pragma unroll
+    for (int r = 0; r < RP; r += 4)
+      *reinterpret_cast<float4*>(Cl + k * CP + r) = make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
+  }
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) El[b] = E_.e[b];
+  if (threadIdx.x == 0) {
+    const float nrm = sqrtf(st->normsq_s);
+    sc.coef = nrm > 0.0f ? lambda_s / nrm : 0.0f;
+    sc.as = adam_scalars(ad, st->step_s + 1);
+    if (blockIdx.x == 0) {
+      // book-keeping of spass_kernel (mode 1)
+      int pend = st->pending;
+      if (pend & QSC_PEND_C) st->step_c += 1;
+      pend &= ~QSC_PEND_C;
+      st->pending = pend | QSC_PEND_SNLL | QSC_PEND_SUPD;
+      st->normsq_s_prev = st->normsq_s;
+      st->iter += 1;
+    }
+  }
+  __syncthreads();
+
+  // 2. S-step over the wave's slices (next slice's reads in flight)
+  for (int n = 0; il < nsl; ++n) {
+    const int il1 = local_of(n + 1);
+    const bool more = il1 < nsl;
+    const int s = global_of(il);
+    SliceIn<RP, E, ADAM> nxt;
+    slice_load(nxt, s_ent, s_width, s_off, more ? global_of(il1) : s, p, h, S, mS, vS);
+    float sv[RP];
+#pragma unroll
+    for (int r = 0; r < RP; ++r) sv[r] = cur.sv[r];
+    f2v own[RP / 2];
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j) own[j] = f2v{sv[2 * j], sv[2 * j + 1]} * splat2(own_scale);
+    f2v accp[RP / 2];
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
+    float nll = 0.0f;
+    walk_groups<RP, E, KIND, LOG>(cur.src, QSC_SLICE, h, cur.j1, 2, cur.buf, own, Cl, El, lk,
+                                  accp, nll);
+    float acc[RP];
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j) {
+      acc[2 * j] = half_sum(accp[j].x);
+      acc[2 * j + 1] = half_sum(accp[j].y);
+    }
+    float a[RH], pv[RH], m[RH], v[RH], nsq = 0.0f;
+#pragma unroll
+    for (int j = 0; j < RH; ++j) {
+      a[j] = pick(hmask, acc[j], acc[RH + j]);
+      pv[j] = pick(hmask, sv[j], sv[RH + j]);
+      m[j] = cur.mv[j];
+      v[j] = cur.vv[j];
+      const float g = __fadd_rn(a[j], __fmul_rn(pv[j], sc.coef));
+      adam_elem_fast(pv[j], m[j], v[j], g, sc.as);
+      nsq = __builtin_fmaf(pv[j], pv[j], nsq);
+    }
+    const int64_t row = ((int64_t)s * QSC_SLICE + p) * RP;
+    st_row<RH>(S + row + h * RH, pv);
+    st_row<RH>(mS + row + h * RH, m);
+    st_row<RH>(vS + row + h * RH, v);
+    st_row<RH>(Sl + (il * QSC_SLICE + p) * CP + h * RH, pv);  // the tile row, for the C-pass
+    nsq = wave_sum_dpp(nsq);
+    if (lane == 0) part_nsq_s[s] = nsq;
+    nll = wave_sum_dpp(nll) * kLn2;
+    if (lane == 0) part_nll_s[s] = nll;
+    if (!more) break;
+    cur.assign(nxt);
+    il = il1;
+  }
+
+  // 3. C-pass units of the tile at the new S (cpass_tile_kernel steps 1, 3, 4)
+  int u = w;
+  V4 buf[kGroup];
+  float cv[RP];
+  int wi = 0, j0 = 0, j1 = 0;
+  const V4* src = nullptr;
+  auto unit_begin = [&](int uu) {
+    const int ks = uu / NP, part = uu - ks * NP;
+    wi = t * nks + ks;
+    const int W4 = c_width[wi] >> 2;
+    j0 = (W4 * part) / NP;
+    j1 = (W4 * (part + 1)) / NP;
+    src = reinterpret_cast<const V4*>(c_ent + c_off[wi]) + lane;
+    load_group(src, 64, j0, 1, max(j1 - 1, 0), buf);
+    const int k = min(ks * 64 + lane, K - 1);
+#pragma unroll
+    for (int r = 0; r < RP; ++r) cv[r] = Cl[k * CP + r];  // C_i, as the S-step used
+  };
+  if (u < U) unit_begin(u);
+  __syncthreads();  // the whole S tile is in LDS
+  for (; u < U; u += NW) {
+    const int ks = u / NP;
+    const int k = ks * 64 + lane;
+    f2v own[RP / 2];
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j)
+      own[j] = f2v{(2 * j < R && k < K) ? cv[2 * j] : 0.0f,
+                   (2 * j + 1 < R && k < K) ? cv[2 * j + 1] : 0.0f} * splat2(own_scale);
+    f2v accp[RP / 2];
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
+    float nll = 0.0f;
+    walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+    nll = wave_sum_dpp(nll) * kLn2;
+    if (NP == 1) {
+#pragma unroll
+      for (int j = 0; j < RP / 2; ++j) {
+        if (2 * j < R) slab[((int64_t)t * R + 2 * j) * Kp + k] = accp[j].x;
+        if (2 * j + 1 < R) slab[((int64_t)t * R + 2 * j + 1) * Kp + k] = accp[j].y;
+      }
+      if (lane == 0) part_nll_c[wi] = nll;
+    } else {
+#pragma unroll
+      for (int j = 0; j < RP / 2; ++j) {
+        if (2 * j < R) Pl[((size_t)u * R + 2 * j) * 64 + lane] = accp[j].x;
+        if (2 * j + 1 < R) Pl[((size_t)u * R + 2 * j + 1) * 64 + lane] = accp[j].y;
+      }
+      if (lane == 0) Nl[u] = nll;
+    }
+    if (u + NW < U) unit_begin(u + NW);
+  }
+  if (NP > 1) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nks * R * 64; i += blockDim.x) {
+      const int ks = i / (R * 64), rl = i - ks * (R * 64);
+      const float* pp0 = Pl + (size_t)ks * NP * R * 64 + rl;
+      float acc = pp0[0];
+      for (int pp = 1; pp < NP; ++pp) acc += pp0[(size_t)pp * R * 64];
+      const int r = rl >> 6, l = rl & 63;
+      slab[((int64_t)t * R + r) * Kp + ks * 64 + l] = acc;
+    }
+    for (int ks = threadIdx.x; ks < nks; ks += blockDim.x) {
+      float acc = Nl[ks * NP];
+      for (int pp = 1; pp < NP; ++pp) acc += Nl[ks * NP + pp];
+      part_nll_c[t * nks + ks] = acc;
+    }
+  }
+  if (blockIdx.x == 0) {
+    __syncthreads();
+    const float nsq = cnorm_sq(C, R * K, Nl);
+    if (threadIdx.x == 0) *cnsq = nsq;
+  }
+}
+
+// LDS bytes of scfused_kernel
+size_t scfused_lds(int PT, int R, int K, int nks, int NP) {
+  const int RP = R <= 4 ? 4 : (R <= 8 ? 8 : 16);
+  const int CP = RP == 4 ? 4 : RP + 4;
+  const size_t U = (size_t)nks * NP;
+  return 32 + (size_t)K * CP * 4 + 256 * 8 + (size_t)PT * CP * 4 +
+         (NP > 1 ? U * R * 64 * 4 : 0) + std::max<size_t>(U, 16) * 4;
+}
+
+// ---------------------------------------------------------------------------------------
 // book-keeping shared by cfinish (block 0) and state_flush: settle a pending S-pass
 // ---------------------------------------------------------------------------------------
 __device__ void settle_s(qsc_state* __restrict__ st, const float* __restrict__ part_nll_s,
@@ -1330,6 +1537,67 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
                      d->nbins, R, d->K, S, C, w.slab, w.cnll, w.cnsq)
   QSC_DISPATCH_PASS(CPASS_LAUNCH);
 #undef CPASS_LAUNCH
+  QSC_CHECK_LAUNCH();
+  return QSC_OK;
+}
+
+// fused S-step + next C-pass: the C-pass tile partition (NP parts per bin list) of qsc_cpass
+static int cpass_parts(const qsc_obs_desc* d) {
+  const int nks = d->nks;
+  int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
+  const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
+  while (NP > 1 && chunks / NP < 3.0) --NP;
+  return NP;
+}
+
+QSC_API int qsc_scpass_supported(const qsc_obs_desc* d, int32_t R) {
+  if (!desc_ok(d) || R < 1 || R > 8) return 0;
+  const int NP = cpass_parts(d);
+  const int U = d->nks * NP;
+  return (U >= 4 && U <= QSC_CTILE_MAXW && d->PT <= 4096 &&
+          scfused_lds(d->PT, R, d->K, d->nks, NP) <= 160 * 1024)
+             ? 1
+             : 0;
+}
+
+QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
+                       const int64_t* s_off, const void* c_entries, const int32_t* c_width,
+                       const int64_t* c_off, const qsc_model* m, int32_t R, float* S,
+                       const float* C, float* mS, float* vS, const qsc_adam* adam,
+                       float lambda_s, qsc_state* st, void* ws, size_t ws_bytes, void* stream) {
+  if (!qsc_scpass_supported(d, R) || !m || m->nbounds - 1 != d->nbins || !S || !C || !mS ||
+      !vS || !adam || !st || !s_width || !s_off || !c_width || !c_off ||
+      (d->s_entries > 0 && !s_entries) || (d->c_entries > 0 && !c_entries) || !ws ||
+      ws_bytes < ws_bytes_for(d, R))
+    return QSC_EINVAL;
+  const int RP = rp_of(R);
+  const int NP = cpass_parts(d);
+  const size_t shm = scfused_lds(d->PT, R, d->K, d->nks, NP);
+  PassWs w = carve(d, R, ws);
+  Edges E;
+  make_edges(m, &E);
+  const Lik lk = make_lik(m);
+  const int kind = lik_kind(m);
+  if (kind == LIK_SQUARED)
+    make_sq_targets(m, &E);
+  else if (!m->log_model)
+    scale_edges(&E, m->nbounds - 1, lk.a);
+  const qsc_adam ad = *adam;
+  // waves: two S-step slices each (the tile's nsl slices), 4..16
+  const int nsl = d->PT / QSC_SLICE;
+  const unsigned threads = 64u * (unsigned)std::min(16, std::max(4, nsl / 2));
+  hipStream_t s = STREAM(stream);
+#define SCPASS_LAUNCH(RPV, ET, KD, LG)                                                         \
+  do {                                                                                         \
+    if constexpr (RPV <= 8)                                                                    \
+      hipLaunchKernelGGL((scfused_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles),         \
+                         dim3(threads), shm, s, (const ET*)s_entries, s_width, s_off,         \
+                         (const ET*)c_entries, c_width, c_off, d->nks, NP, d->PT, lk, E,       \
+                         d->nbins, R, d->K, S, C, mS, vS, ad, lambda_s, st, w.snll, w.snsq,    \
+                         w.slab, w.cnll, w.cnsq);                                              \
+  } while (0)
+  QSC_DISPATCH_PASS(SCPASS_LAUNCH);
+#undef SCPASS_LAUNCH
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }

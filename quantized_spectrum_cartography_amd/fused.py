@@ -68,6 +68,18 @@ class PassEngine:
                   _lib.ptr(mS), _lib.ptr(vS), adam, float(lambda_s), _lib.ptr(self.state),
                   _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
 
+    def scpass_supported(self):
+        return bool(_lib.lib().qsc_scpass_supported(self.obs.desc, self.R))
+
+    def scpass(self, S_pos, C, mS, vS, adam, lambda_s):
+        """spass (mode 1, Adam) fused with the next cpass at the updated S (qsc_scpass)."""
+        o = self.obs
+        _lib.call("qsc_scpass", o.desc, _lib.ptr(o.s_entries), _lib.ptr(o.s_width),
+                  _lib.ptr(o.s_off), _lib.ptr(o.c_entries), _lib.ptr(o.c_width),
+                  _lib.ptr(o.c_off), o.model, self.R, _lib.ptr(S_pos), _lib.ptr(C), _lib.ptr(mS),
+                  _lib.ptr(vS), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),
+                  self.ws.numel(), _lib.stream())
+
     def supdate(self, S_pos, mS, vS, g, adam, lambda_s):
         _lib.call("qsc_supdate", self.obs.desc, self.R, _lib.ptr(S_pos), _lib.ptr(mS), _lib.ptr(vS),
                   _lib.ptr(g), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),

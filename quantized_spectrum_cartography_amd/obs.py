@@ -6,6 +6,8 @@ into uint8 codes (0xFF = unobserved), then packs only the observed entries into 
 sliced formats of include/qsc.h (one per pass), with pixels re-ordered by observation count
 so that the 64 lanes of every wavefront carry near-equal work.  Built once per solve.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -18,6 +20,8 @@ def default_tile(P, R, K):
     The C-pass runs one 4-wave workgroup per (tile, 64-bin slice): aim for ~1024 workgroups
     (4 per CU) while keeping tiles large, since the per-bin lists of a tile are padded to their
     longest (bigger tiles -> relatively less padding) and the tile's S rows live in LDS."""
+    if os.environ.get("QSC_CTILE"):  # tuning override (power of two, 64..4096)
+        return int(os.environ["QSC_CTILE"])
     Pp = -(-P // 64) * 64
     nks = -(-K // 64)
     want = max(1, (Pp * nks) // 1024)

@@ -40,12 +40,15 @@ class FreeSSolver:
     """Device-resident free-S alternating solver over one Observations set.
 
     State (position-ordered S, Adam moments, step counters, ||S||^2, NLLs) lives on the GPU.
-    `run(n)` issues 4 launches per iteration; with `use_graph` the iteration is captured once
-    in a hipGraph (torch.cuda.CUDAGraph) and replayed.
+    An iteration is cpass, cfinish (C-step) then spass (S-step).  With `fuse` (default where
+    qsc_scpass_supported) `run(n)` issues the same kernel sequence with each S-step and the
+    following C-pass in one launch: cpass, cfinish, (scpass, cfinish) x (n-1), spass -- two
+    launches per iteration.  With `use_graph` the repeated body is captured once in a hipGraph
+    (torch.cuda.CUDAGraph) and replayed.
     """
 
     def __init__(self, obs, S_init, C_init, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
-                 betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024):
+                 betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024, fuse=True):
         self.obs = obs
         R = S_init.shape[0]
         self.R = R
@@ -60,6 +63,9 @@ class FreeSSolver:
         self.engine.init_state(self.S)
         self._graph = None
         self._graph_iters = 0
+        self.fuse = bool(fuse) and self.engine.scpass_supported()
+        self._fgraph = None
+        self._fgraph_iters = 0
 
     # one outer iteration = C grad-step + S grad-step
     def c_step(self):
@@ -75,6 +81,23 @@ class FreeSSolver:
         self.c_step()
         self.s_step()
 
+    def fused_body(self):
+        """S-step i fused with C-pass i+1, then C-step i+1's finish (needs a C-step before)."""
+        e = self.engine
+        e.scpass(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s)
+        e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)
+
+    def _capture_fused(self, iters):
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(iters):
+                    self.fused_body()
+        torch.cuda.current_stream().wait_stream(s)
+        self._fgraph, self._fgraph_iters = g, iters
+
     def capture(self, iters=1):
         """Capture `iters` iterations into one graph (replayed by run)."""
         g = torch.cuda.CUDAGraph()
@@ -88,6 +111,20 @@ class FreeSSolver:
         self._graph, self._graph_iters = g, iters
 
     def run(self, n, use_graph=False):
+        if self.fuse and n >= 2:
+            self.c_step()
+            m = n - 1
+            if use_graph:
+                if self._fgraph is None:
+                    self._capture_fused(1 if m < 8 else 8)
+                k = m // self._fgraph_iters
+                for _ in range(k):
+                    self._fgraph.replay()
+                m -= k * self._fgraph_iters
+            for _ in range(m):
+                self.fused_body()
+            self.s_step()
+            return
         if use_graph:
             if self._graph is None:
                 self.capture(1 if n < 8 else 8)
@@ -126,7 +163,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
           log_model=False, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2, max_iter=500,
           betas=(0.9, 0.999), eps=1e-8, project_c=True, generator=None, Z_init=None,
           restart=False, restart_samples=(200, 200), T_true=None, nmse_every=0,
-          use_graph=False, obs=None, tile=None, callback=None, loss="probit"):
+          use_graph=False, obs=None, tile=None, callback=None, loss="probit", fuse=True):
     """Alternating S/C probit-MLE (qmc/qmc.ipynb :559-645).
 
     Args mirror the notebook globals: Y (K,1,I,J) bin indices, Wx (K,1,I,J) 0/1 mask,
@@ -152,7 +189,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
         if S_init is None:
             S_init = torch.zeros(R, 1, I, J)
         sol = FreeSSolver(obs, S_init, C_init, lambda_c, lambda_s, lr_c, lr_s, betas, eps,
-                          project_c, hist_cap=max_iter)
+                          project_c, hist_cap=max_iter, fuse=fuse)
         nmse = []
         done = 0
         chunk = nmse_every if (nmse_every and T_true is not None) else max_iter

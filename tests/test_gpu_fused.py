@@ -139,6 +139,35 @@ def test_solver_graph_replay_matches_eager():
     assert np.array_equal(a.C.cpu().numpy(), b.C.cpu().numpy())
 
 
+@pytest.mark.parametrize("seed,R,I,J,K,log_model,loss", [(41, 4, 64, 64, 64, False, "probit"),
+                                                       (42, 8, 96, 80, 256, False, "probit"),
+                                                       (43, 3, 50, 70, 130, False, "probit"),
+                                                       (44, 5, 64, 64, 64, False, "squared"),
+                                                       (46, 4, 64, 64, 64, True, "probit")])
+def test_fused_spass_cpass_bitexact(seed, R, I, J, K, log_model, loss):
+    """qsc_scpass (S-step + next C-pass in one launch) reproduces spass + cpass bit for bit:
+    S, C and the cost history after n iterations, eager and hipGraph."""
+    from quantized_spectrum_cartography_amd import qmc
+    d = _random_case(seed, R, I, J, K, log_model=log_model)
+    kw = dict(S_init=d["S0"], C_init=d["C0"], max_iter=11, loss=loss, offset=d["offset"],
+              log_model=log_model)
+    a = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], fuse=False, **kw)
+    for g in (False, True):
+        b = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], fuse=True, use_graph=g, **kw)
+        assert np.array_equal(a.S.cpu().numpy(), b.S.cpu().numpy())
+        assert np.array_equal(a.C.cpu().numpy(), b.C.cpu().numpy())
+        assert a.costs_c == b.costs_c and a.costs_s == b.costs_s
+
+
+def test_fused_solver_is_used():
+    from quantized_spectrum_cartography_amd import obs as obs_mod
+    from quantized_spectrum_cartography_amd.qmc import FreeSSolver
+    d = _random_case(45, 8, 64, 64, 256)
+    o = obs_mod.Observations(d["Y"], d["Wx"], d["b"], d["sigma"])
+    assert FreeSSolver(o, d["S0"], d["C0"]).fuse
+    assert not FreeSSolver(o, d["S0"], d["C0"], fuse=False).fuse
+
+
 def test_solver_vs_oracle_random_sizes():
     from quantized_spectrum_cartography_amd import qmc
     for seed, R, I, J, K in [(31, 3, 37, 29, 90), (32, 8, 64, 64, 256)]:
