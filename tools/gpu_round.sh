@@ -26,7 +26,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $G/prof -o run --output-fo
 tail -1 $G/bench_prof.log
 if [ -z "$NO_PMC" ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 240 rocprofv3 --pmc $c --kernel-include-regex "spass|cpass|cfinish" -d $G/pmc_$c -o run --output-format csv -- python3 $R/tools/prof_passes.py --iters 20 > $G/pmc_$c.log 2>&1 || stop $? pmc_$c
+    timeout -s KILL 240 rocprofv3 --pmc $c --kernel-include-regex "scfused|spass|cpass|cfinish" -d $G/pmc_$c -o run --output-format csv -- python3 $R/tools/prof_passes.py --iters 20 > $G/pmc_$c.log 2>&1 || stop $? pmc_$c
     echo "pmc $c ok"
   done
 fi

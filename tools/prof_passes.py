@@ -24,10 +24,12 @@ def main():
     prob = synthetic.onebit_problem(I, J, K, R, seed=20263, keep_T=False)
     obs = Observations(prob["Y"], prob["Wx"], prob["b"], prob["sigma"], R_hint=R)
     print("obs", obs.stats(), flush=True)
-    sol = FreeSSolver(obs, prob["S0"], prob["C0"], hist_cap=args.iters + 4)
-    sol.run(args.iters)
-    torch.cuda.synchronize()
-    print("done", sol.state(), flush=True)
+    # the three-launch form (warm spass / cpass dispatches), then the fused form (scfused)
+    for fuse in (False, True):
+        sol = FreeSSolver(obs, prob["S0"], prob["C0"], hist_cap=args.iters + 4, fuse=fuse)
+        sol.run(args.iters)
+        torch.cuda.synchronize()
+        print("done fuse=%s" % fuse, sol.state(), flush=True)
 
 
 if __name__ == "__main__":
