@@ -51,9 +51,10 @@ def kslab_observations(Y_local, Wx_local, bin_boundaries, noise_std, dist, offse
                         log_model=log_model, tile=tile, R_hint=R_hint, count_hook=hook)
 
 
-def _capture(solver, iters):
+def _capture(solver, iters, body=None):
     """Capture `iters` iterations (kernels + RCCL collectives) in one hipGraph; None if the
     backend refuses capture (the solver then runs eagerly)."""
+    body = body or solver.iteration
     try:
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream()
@@ -61,7 +62,7 @@ def _capture(solver, iters):
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
                 for _ in range(iters):
-                    solver.iteration()
+                    body()
         torch.cuda.current_stream().wait_stream(s)
         return g
     except Exception:  # pragma: no cover - depends on the RCCL build
@@ -69,7 +70,32 @@ def _capture(solver, iters):
         return None
 
 
+def _run_fused(solver, n, use_graph):
+    """C-step, then (S-step i + C-pass i+1 in one launch, the C finish / exchange) x (n-1), then
+    the last S-step: the kernel sequence of n plain iterations (FreeSSolver.run)."""
+    solver.c_step()
+    m = n - 1
+    if use_graph and torch.cuda.is_available() and solver.S.is_cuda:
+        if solver._fgraph is None and not solver._graph_failed:
+            gi = 1 if m < 8 else 8
+            g = _capture(solver, gi, solver.fused_body)
+            if g is None:
+                solver._graph_failed = True
+            else:
+                solver._fgraph, solver._fgraph_iters = g, gi
+        if solver._fgraph is not None:
+            k = m // solver._fgraph_iters
+            for _ in range(k):
+                solver._fgraph.replay()
+            m -= k * solver._fgraph_iters
+    for _ in range(m):
+        solver.fused_body()
+    solver.s_step()
+
+
 def _run(solver, n, use_graph):
+    if getattr(solver, "fuse", False) and n >= 2:
+        return _run_fused(solver, n, use_graph)
     if use_graph and torch.cuda.is_available() and solver.S.is_cuda:
         if solver._graph is None and not solver._graph_failed:
             gi = 1 if n < 8 else 8
@@ -92,7 +118,7 @@ class IJSlabSolver:
 
     def __init__(self, obs, S_init_local, C_init, dist, lambda_c=100.0, lambda_s=100.0,
                  lr_c=5e-3, lr_s=1e-2, betas=(0.9, 0.999), eps=1e-8, project_c=True,
-                 hist_cap=1024, engine=None):
+                 hist_cap=1024, engine=None, fuse=True):
         self.obs, self.dist = obs, dist
         R = S_init_local.shape[0]
         self.R = R
@@ -112,14 +138,26 @@ class IJSlabSolver:
         self.lambda_c, self.lambda_s = float(lambda_c), float(lambda_s)
         self.engine.init_state(self.S)
         self._graph, self._graph_iters, self._graph_failed = None, 0, False
+        # S-step + next C-pass in one launch (qsc_scpass), as FreeSSolver
+        sup = getattr(self.engine, "scpass_supported", None)
+        self.fuse = bool(fuse) and sup is not None and bool(sup())
+        self._fgraph, self._fgraph_iters = None, 0
 
-    def c_step(self):
+    def fused_body(self):
+        """S-step i + C-pass i+1 (one launch), then C-step i+1's exchange and update."""
+        self.engine.scpass(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s)
+        self._c_exchange()
+
+    def _c_exchange(self):
         e = self.engine
-        e.cpass(self.S, self.C)
         e.cfinish(self.C, 2, dC=self.red)
         self.dist.all_reduce(self.red)
         e.cupdate(self.C, self.mC, self.vC, self.red, self.adam_c, self.lambda_c,
                   normsq_s_ext=self.red[self.R * self.obs.K:])
+
+    def c_step(self):
+        self.engine.cpass(self.S, self.C)
+        self._c_exchange()
 
     def s_step(self):
         self.engine.spass(self.S, self.C, 1, mS=self.mS, vS=self.vS, adam=self.adam_s,

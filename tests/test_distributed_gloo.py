@@ -53,6 +53,7 @@ class _CpuEngine:
         self.hist_cap = 0
         self.hist = torch.zeros(4)
         self.st = dict(step_c=0, step_s=0, iter=0, normsq_s=0.0, nll_c=0.0, nll_s=0.0)
+        self.calls = []
 
     def _grad(self, S, C):
         return explicit.nll_grad(S.double().numpy(), C.double().numpy(), self.obs.Y, self.obs.Wx,
@@ -111,6 +112,15 @@ class _CpuEngine:
         self.st["step_s"] += 1
         self._adam(S, mS, vS, gg, self.st["step_s"], adam)
         self.st["normsq_s"] = float((S.double() ** 2).sum())  # this shard's, settled later
+
+    def scpass_supported(self):
+        return True
+
+    def scpass(self, S, C, mS, vS, adam, lambda_s):
+        """qsc_scpass: the S-step, then the next C-pass at the updated S."""
+        self.calls.append("scpass")
+        self.spass(S, C, 1, mS=mS, vS=vS, adam=adam, lambda_s=lambda_s)
+        self.cpass(S, C)
 
     def supdate(self, S, mS, vS, g, adam, lambda_s):
         nrm = math.sqrt(self.st["normsq_s"])
@@ -245,3 +255,19 @@ def test_ijslab_two_ranks_match_single_process(tmp_path):
     ref = osolver.free_s_solve(S0, C0, Y, Wx, b, sigma, n_iter=ITERS)
     assert rel_fro(S_two.reshape(R, -1), ref["S"].reshape(R, -1).numpy()) < 1e-5
     assert rel_fro(r0["C"], ref["C"].numpy()) < 1e-5
+
+
+def test_ijslab_fused_sequence_equals_plain():
+    """IJ-slab with the fused launch (S-step i + C-pass i+1, qsc_scpass) runs the same kernel
+    sequence as plain iterations: cpass, exchange, (scpass, exchange) x (n-1), spass."""
+    from quantized_spectrum_cartography_amd.distributed import IJSlabSolver
+    S0, C0, Y, Wx, b, sigma = _problem()
+    out = []
+    for fuse in (True, False):
+        eng = _CpuEngine(_Obs(Y, Wx), b.numpy(), sigma)
+        sol = IJSlabSolver(_Obs(Y, Wx), S0, C0, dist=_SoloDist, engine=eng, fuse=fuse)
+        assert sol.fuse == fuse
+        sol.run(ITERS)
+        out.append((sol.S.clone(), sol.C.clone(), eng.calls.count("scpass")))
+    assert out[0][2] == ITERS - 1 and out[1][2] == 0
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
