@@ -139,16 +139,19 @@ def test_solver_graph_replay_matches_eager():
     assert np.array_equal(a.C.cpu().numpy(), b.C.cpu().numpy())
 
 
-@pytest.mark.parametrize("seed,R,I,J,K,log_model,loss", [(41, 4, 64, 64, 64, False, "probit"),
-                                                       (42, 8, 96, 80, 256, False, "probit"),
-                                                       (43, 3, 50, 70, 130, False, "probit"),
-                                                       (44, 5, 64, 64, 64, False, "squared"),
-                                                       (46, 4, 64, 64, 64, True, "probit")])
-def test_fused_spass_cpass_bitexact(seed, R, I, J, K, log_model, loss):
+@pytest.mark.parametrize("seed,R,I,J,K,log_model,loss,nbins",
+                         [(41, 4, 64, 64, 64, False, "probit", 2),
+                          (42, 8, 96, 80, 256, False, "probit", 2),
+                          (43, 3, 50, 70, 130, False, "probit", 2),
+                          (44, 5, 64, 64, 64, False, "squared", 2),
+                          (46, 4, 64, 64, 64, True, "probit", 2),
+                          (47, 6, 40, 56, 100, False, "probit", 20),   # wide (uint32) entries
+                          (48, 1, 33, 31, 70, False, "probit", 2)])    # R = 1, ragged P, K
+def test_fused_spass_cpass_bitexact(seed, R, I, J, K, log_model, loss, nbins):
     """qsc_scpass (S-step + next C-pass in one launch) reproduces spass + cpass bit for bit:
     S, C and the cost history after n iterations, eager and hipGraph."""
     from quantized_spectrum_cartography_amd import qmc
-    d = _random_case(seed, R, I, J, K, log_model=log_model)
+    d = _random_case(seed, R, I, J, K, nbins=nbins, log_model=log_model)
     kw = dict(S_init=d["S0"], C_init=d["C0"], max_iter=11, loss=loss, offset=d["offset"],
               log_model=log_model)
     a = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], fuse=False, **kw)
