@@ -9,6 +9,8 @@ differentiates:
 Scalars (step counters, ||S||^2, NLLs, the cost history) stay on the device and their
 book-keeping rides on those same kernels (qsc_state protocol in include/qsc.h), so an outer
 iteration is three launches with no host synchronisation and is captured in one hipGraph.
+qsc_scpass runs an S-step and the following C-pass as one launch (the C-pass of iteration i+1
+reads only its tile's S_i, handed over in LDS), so solvers issue two launches per iteration.
 """
 import torch
 
