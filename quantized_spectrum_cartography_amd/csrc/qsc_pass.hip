@@ -905,12 +905,36 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
   // this wave's n-th slice of the tile (local index) and its global slice
   auto local_of = [&](int n) { return n * NW + ((n & 1) ? (NW - 1 - w) : w); };
   auto global_of = [&](int i) { return i * nt + ((i & 1) ? (nt - 1 - t) : t); };
+  [[maybe_unused]] const int wg = blockIdx.x * (kCTBlock / 64) + w;  // (diagnostic stamps)
+  STAMP(wg, 0);
+  RSTAMP(wg, 28);
 
-  // 1. first slice's reads, then C^T + edges into LDS
+  // 1. C^T / edge / state reads first (the LDS staging then waits only for them: vmcnt
+  //    retires in issue order), then the first slice's reads, then the staging
+  const int k0 = threadIdx.x;
+  float c0[RP];
+#pragma unroll
+  for (int r = 0; r < RP; ++r) c0[r] = C[(int64_t)min(r, R - 1) * K + min(k0, K - 1)];
+  const float2 e0 = E_.e[min(k0, nbins - 1)];
+  float nsq_s = 0.0f;
+  int step_s = 0;
+  if (threadIdx.x == 0) {
+    nsq_s = st->normsq_s;
+    step_s = st->step_s;
+  }
+  __builtin_amdgcn_sched_barrier(0);
   int il = local_of(0);
   SliceIn<RP, E, ADAM> cur;
   slice_load(cur, s_ent, s_width, s_off, global_of(il < nsl ? il : 0), p, h, S, mS, vS);
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+  {
+    const int kw = min(k0, K - 1);  // branch-free: threads past K rewrite row K-1
+#pragma unroll
+    for (int r = 0; r < RP; r += 4)
+      *reinterpret_cast<float4*>(Cl + kw * CP + r) =
+          make_float4(r < R ? c0[r] : 0.0f, r + 1 < R ? c0[r + 1] : 0.0f,
+                      r + 2 < R ? c0[r + 2] : 0.0f, r + 3 < R ? c0[r + 3] : 0.0f);
+  }
+  for (int k = k0 + (int)blockDim.x; k < K; k += blockDim.x) {
     float v[RP];
 #pragma unroll
     for (int r = 0; r < RP; ++r) v[r] = (r < R) ? C[(int64_t)r * K + k] : 0.0f;
@@ -918,22 +942,24 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
     for (int r = 0; r < RP; r += 4)
       *reinterpret_cast<float4*>(Cl + k * CP + r) = make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
   }
-  for (int b = threadIdx.x; b < nbins; b += blockDim.x) El[b] = E_.e[b];
+  El[min(k0, nbins - 1)] = e0;
+  for (int b = k0 + (int)blockDim.x; b < nbins; b += blockDim.x) El[b] = E_.e[b];
   if (threadIdx.x == 0) {
-    const float nrm = sqrtf(st->normsq_s);
+    const float nrm = sqrtf(nsq_s);
     sc.coef = nrm > 0.0f ? lambda_s / nrm : 0.0f;
-    sc.as = adam_scalars(ad, st->step_s + 1);
+    sc.as = adam_scalars(ad, step_s + 1);
     if (blockIdx.x == 0) {
       // book-keeping of spass_kernel (mode 1)
       int pend = st->pending;
       if (pend & QSC_PEND_C) st->step_c += 1;
       pend &= ~QSC_PEND_C;
       st->pending = pend | QSC_PEND_SNLL | QSC_PEND_SUPD;
-      st->normsq_s_prev = st->normsq_s;
+      st->normsq_s_prev = nsq_s;
       st->iter += 1;
     }
   }
   __syncthreads();
+  STAMP(wg, 1);
 
   // 2. S-step over the wave's slices (next slice's reads in flight)
   for (int n = 0; il < nsl; ++n) {
@@ -1003,8 +1029,10 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
 #pragma unroll
     for (int r = 0; r < RP; ++r) cv[r] = Cl[k * CP + r];  // C_i, as the S-step used
   };
+  STAMP(wg, 2);
   if (u < U) unit_begin(u);
   __syncthreads();  // the whole S tile is in LDS
+  STAMP(wg, 3);
   for (; u < U; u += NW) {
     const int ks = u / NP;
     const int k = ks * 64 + lane;
@@ -1036,6 +1064,7 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
     }
     if (u + NW < U) unit_begin(u + NW);
   }
+  STAMP(wg, 4);
   if (NP > 1) {
     __syncthreads();
     for (int i = threadIdx.x; i < nks * R * 64; i += blockDim.x) {
@@ -1057,6 +1086,8 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
     const float nsq = cnorm_sq(C, R * K, Nl);
     if (threadIdx.x == 0) *cnsq = nsq;
   }
+  STAMP(wg, kStampLast);
+  RSTAMP(wg, 29);
 }
 
 // LDS bytes of scfused_kernel
