@@ -1172,6 +1172,14 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
 
   const int r = blockIdx.x / nks, ks = blockIdx.x - r * nks;
   const int k = ks * 64 + lane;
+  // wave 0 reads its C / moments ahead of the tile sum (one HBM round trip instead of two)
+  float p0 = 0.0f, m0 = 0.0f, v0 = 0.0f;
+  if (mode == 1 && wave == 0 && k < K) {
+    const int64_t i = (int64_t)r * K + k;
+    p0 = C[i];
+    m0 = mC[i];
+    v0 = vC[i];
+  }
   if (threadIdx.x == 0 && mode == 1) {
     const float nrm = sqrtf(nsq);
     sc.coef = nrm > 0.0f ? lambda_c / nrm : 0.0f;
@@ -1200,7 +1208,7 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
     for (int w = 1; w < NW; ++w) g += red[w][lane];
     const int64_t i = (int64_t)r * K + k;
     if (mode == 1) {
-      float p = C[i], m = mC[i], v = vC[i];
+      float p = p0, m = m0, v = v0;
       g = __fadd_rn(g, __fmul_rn(p, sc.coef));
       adam_elem(p, m, v, g, ad, sc.as);
       C[i] = p;
