@@ -1154,12 +1154,63 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
   const float nsq = normsq_ext ? *normsq_ext : *cnsq;
 
   if (blockIdx.x == R * nks) {
-    // book-keeping block: settle the S-pass partials and total the C-pass NLL
-    settle_s(st, part_nll_s, part_nsq_s, nslices, hist, hist_cap, shn);
-    float s = 0.0f;
-    for (int i = threadIdx.x; i < npart_c; i += blockDim.x) s += part_nll_c[i];
-    const float tot = block_sum(s, shn);
+    // book-keeping block: settle the S-pass partials (settle_s) and total the C-pass NLL.
+    // Every partial is read up front (one memory round trip, batches of 8 loads in flight)
+    // and the three fixed-order block sums share one LDS pass; same sums, same order as
+    // settle_s + block_sum.
+    __shared__ float sh3[3][NW];
+    const int pend = st->pending;
+    const bool settle = (pend & (QSC_PEND_SNLL | QSC_PEND_SUPD)) != 0;
+    const bool supd = (pend & QSC_PEND_SUPD) != 0;
+    float a = 0.0f, b = 0.0f, c = 0.0f;
+    const int step = blockDim.x;
+    for (int i0 = threadIdx.x; settle && i0 < nslices; i0 += 8 * step) {
+      float va[8], vb[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = min(i0 + j * step, nslices - 1);
+        va[j] = part_nll_s[i];
+        vb[j] = supd ? part_nsq_s[i] : 0.0f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (i0 + j * step < nslices) {
+          a += va[j];
+          if (supd) b += vb[j];
+        }
+    }
+    for (int i = threadIdx.x; i < npart_c; i += blockDim.x) c += part_nll_c[i];
+    a = wave_sum(a);
+    b = wave_sum(b);
+    c = wave_sum(c);
+    if (lane == 0) {
+      sh3[0][wave] = a;
+      sh3[1][wave] = b;
+      sh3[2][wave] = c;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
+      float sn = 0.0f, sq = 0.0f, tot = 0.0f;
+      for (int w = 0; w < NW; ++w) {
+        sn += sh3[0][w];
+        sq += sh3[1][w];
+        tot += sh3[2][w];
+      }
+      if (settle) {  // settle_s, thread-0 part
+        const int it = st->iter - 1;
+        st->nll_s = sn;
+        if (hist && it >= 0 && it < hist_cap) {
+          hist[4 * it + 0] = st->nll_c;
+          hist[4 * it + 1] = sn;
+          hist[4 * it + 2] = st->normsq_c;
+          hist[4 * it + 3] = st->normsq_s_prev;
+        }
+        if (supd) {
+          st->normsq_s = sq;
+          st->step_s += 1;
+        }
+        st->pending = pend & ~(QSC_PEND_SNLL | QSC_PEND_SUPD);
+      }
       st->nll_c = tot;
       if (mode == 1) {
         st->normsq_c = nsq;
