@@ -960,6 +960,20 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
   }
   __syncthreads();
   STAMP(wg, 1);
+  if (blockIdx.x == 0) {
+    // ||C_i||^2 for the next C update's regulariser, from the staged C^T at the start (as a
+    // chain of dependent global reads at the end it delayed the last workgroup); the order of
+    // cnorm_sq: thread t < 256 accumulates flat indices t, t + 256, ..., then block_sum
+    float s2 = 0.0f;
+    if (threadIdx.x < 256)
+      for (int i = threadIdx.x; i < R * K; i += 256) {
+        const int r = i / K, k = i - r * K;
+        const float c = Cl[k * CP + r];
+        s2 = __builtin_fmaf(c, c, s2);
+      }
+    const float nsq = block_sum(s2, Nl);
+    if (threadIdx.x == 0) *cnsq = nsq;
+  }
 
   // 2. S-step over the wave's slices (next slice's reads in flight)
   for (int n = 0; il < nsl; ++n) {
@@ -1080,11 +1094,6 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
       for (int pp = 1; pp < NP; ++pp) acc += Nl[ks * NP + pp];
       part_nll_c[t * nks + ks] = acc;
     }
-  }
-  if (blockIdx.x == 0) {
-    __syncthreads();
-    const float nsq = cnorm_sq(C, R * K, Nl);
-    if (threadIdx.x == 0) *cnsq = nsq;
   }
   STAMP(wg, kStampLast);
   RSTAMP(wg, 29);
