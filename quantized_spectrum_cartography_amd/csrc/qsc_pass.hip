@@ -341,7 +341,14 @@ __device__ __forceinline__ float half_sum(float x) {
 __device__ __forceinline__ float cnorm_sq(const float* __restrict__ C, int n, float* sh) {
   float s2 = 0.0f;
   if (threadIdx.x < 256)
-    for (int i = threadIdx.x; i < n; i += 256) s2 = __builtin_fmaf(C[i], C[i], s2);
+    for (int i0 = threadIdx.x; i0 < n; i0 += 8 * 256) {  // 8 reads in flight, summed in order
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = C[min(i0 + 256 * j, n - 1)];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (i0 + 256 * j < n) s2 = __builtin_fmaf(v[j], v[j], s2);
+    }
   return block_sum(s2, sh);
 }
 
