@@ -1160,7 +1160,6 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
     const float* __restrict__ part_nsq_s, int nslices, float* __restrict__ hist, int hist_cap) {
   constexpr int NW = kFBlock / 64;
   __shared__ float red[NW][64];
-  __shared__ float shn[NW];
   __shared__ Scalars sc;
   const int Kp = nks * 64;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
