@@ -159,6 +159,13 @@ QSC_API int qsc_device_check(int dev);
  * Y = i for b[i] < x <= b[i+1] (i >= 1, b[-1] = +inf), else 0.                             */
 QSC_API int qsc_quantize(const float* X, const float* noise, int64_t n, const qsc_model* m,
                          int64_t* Y, void* stream);
+/* bin step of quantize alone: Y = i for b[i] < x <= b[i+1] (i >= 1, b[-1] = +inf), else 0, for
+ * observations x already formed by the caller.  The log model's x = log(X + offset) +
+ * randn*std (qmc/quantization_model_log.py:14) is formed on the host with torch's own CPU log,
+ * so that Y is bit-identical to the reference's (ocml logf and ATen's vectorised log differ by
+ * an ulp on some inputs); the binning loop (qml:15-20) runs here.                            */
+QSC_API int qsc_bin_codes(const float* x, int64_t n, const qsc_model* m, int64_t* Y,
+                          void* stream);
 /* prob_probit: qmc/quantization_model.py:22-39, qmc/quantization_model_log.py:23-41.
  * P = F(b[Y+1] - Xhat) - F(b[Y] - Xhat), F(y) = 0.5*(1 + erf(y / fp32(sigma*1.414213))). */
 QSC_API int qsc_prob_probit(const int64_t* Y, const float* Xhat, int64_t n, const qsc_model* m,

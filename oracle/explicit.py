@@ -72,3 +72,82 @@ def adam_step(p, m, v, g, step, lr, beta1=0.9, beta2=0.999, eps=1e-8):
     bc2 = 1 - beta2 ** step
     p = p - (lr / bc1) * m / (np.sqrt(v) / math.sqrt(bc2) + eps)
     return p, m, v
+
+
+# ---------------------------------------------------------------------------------------
+# Observed-entries-only form (for the full-size parity tests: the same closed form evaluated
+# at the nnz observed (k, p) only, so C3 / C4 passes take seconds, not minutes).
+# ---------------------------------------------------------------------------------------
+def observed(Y, Wx):
+    """(kk, pp, yy) of the observed entries of Y (K,P) under the 0/1 mask Wx (K,P)."""
+    Y = np.asarray(Y).reshape(np.asarray(Y).shape[0], -1)
+    Wx = np.asarray(Wx).reshape(Y.shape)
+    kk, pp = np.nonzero(Wx)
+    return kk.astype(np.int64), pp.astype(np.int64), Y[kk, pp].astype(np.int64)
+
+
+def _scatter(kk, pp, g, K, P):
+    from scipy.sparse import csr_matrix
+    return csr_matrix((g, (kk, pp)), shape=(K, P))
+
+
+def nll_grad_obs(S, C, obs, b, sigma, offset=0.0, log_model=False, chunk=1 << 22):
+    """nll_grad restricted to observed entries obs = (kk, pp, yy): identical math (fp64),
+    evaluated in chunks of `chunk` entries to bound host memory."""
+    S = np.asarray(S, np.float64)
+    C = np.asarray(C, np.float64)
+    kk, pp, yy = obs
+    R, P = S.shape
+    K = C.shape[1]
+    e = edges_of(b, log_model)
+    a = sigma * 1.414213
+    nll = 0.0
+    g = np.empty(kk.shape[0], np.float64)
+    for i0 in range(0, kk.shape[0], chunk):
+        k, p, y = kk[i0:i0 + chunk], pp[i0:i0 + chunk], yy[i0:i0 + chunk]
+        t = np.einsum("rn,rn->n", S[:, p], C[:, k])
+        x = np.log(t + offset) if log_model else t
+        u = (e[y + 1] - x) / a
+        w = (e[y] - x) / a
+        Pr = 0.5 * (1 + erf(u)) - 0.5 * (1 + erf(w))
+        with np.errstate(divide="ignore", invalid="ignore"):
+            nll -= float(np.sum(np.log(Pr)))
+            gx = (np.exp(-u * u) - np.exp(-w * w)) / (a * math.sqrt(math.pi) * Pr)
+        g[i0:i0 + chunk] = gx * (1.0 / (t + offset) if log_model else 1.0)
+    G = _scatter(kk, pp, g, K, P)
+    dS = np.asarray((G.T @ C.T).T)   # (R,P) = C @ G
+    dC = np.asarray((G @ S.T).T)     # (R,K) = S @ G^T
+    return nll, dS, dC
+
+
+def explicit_solve(S0, C0, obs, b, sigma, offset=0.0, log_model=False, n_iter=3,
+                   lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2):
+    """The free-S alternating loop (qmc/qmc.ipynb :559-634 with S as the Adam variable,
+    backup/notebooks/onebit_lowrank.ipynb:1230-1236) with closed-form fp64 gradients:
+      C-step: g = dC_nll + lambda_c C/||C|| (0 at C = 0, torch's norm backward); Adam(lr_c);
+              C[C < 0] = 0
+      S-step (at the new C): g = dS_nll + lambda_s S/||S||; Adam(lr_s).
+    Returns (S, C, costs_c, costs_s), costs evaluated before each update as the reference's
+    cost.item()."""
+    S = np.asarray(S0, np.float64).copy()
+    C = np.asarray(C0, np.float64).copy()
+    mS, vS, mC, vC = (np.zeros_like(S), np.zeros_like(S), np.zeros_like(C), np.zeros_like(C))
+    costs_c, costs_s = [], []
+
+    def reg(X, lam):
+        n = float(np.linalg.norm(X))
+        return lam * n, (lam * X / n if n > 0 else np.zeros_like(X))
+
+    for it in range(1, n_iter + 1):
+        nll, _, dC = nll_grad_obs(S, C, obs, b, sigma, offset, log_model)
+        rc, gc = reg(C, lambda_c)
+        rs, _ = reg(S, lambda_s)
+        costs_c.append(nll + rc + rs)
+        C, mC, vC = adam_step(C, mC, vC, dC + gc, it, lr_c)
+        C = np.maximum(C, 0.0)
+        nll, dS, _ = nll_grad_obs(S, C, obs, b, sigma, offset, log_model)
+        rc, _ = reg(C, lambda_c)
+        rs, gs = reg(S, lambda_s)
+        costs_s.append(nll + rc + rs)
+        S, mS, vS = adam_step(S, mS, vS, dS + gs, it, lr_s)
+    return S, C, costs_c, costs_s

@@ -38,10 +38,22 @@ def quantize(X, noise_std, bin_boundaries, offset=None, log_model=False, noise=N
     Reference: qmc/quantization_model.py:8-20, qmc/quantization_model_log.py:9-21.  The noise is
     drawn exactly as the reference draws it, `torch.randn(X.shape)` from torch's global CPU
     generator, so the same seed gives byte-identical Y; pass `noise` to supply it explicitly.
+    Linear model: x = X + noise*std and the binning on the GPU (qsc_quantize).  Log model: x is
+    formed on the host with torch's log, binned on the GPU (qsc_bin_codes), see there.
     """
     out_dev = X.device
     if noise is None:
         noise = torch.randn(X.shape)
+    if log_model:
+        # x = log(X + offset) + randn*std formed with torch's CPU log, the reference's own op
+        # (qmc/quantization_model_log.py:14): ocml's logf differs from ATen's vectorised log by
+        # an ulp on some inputs, which would flip bin indices at edges.  Binning on the GPU.
+        x = torch.log(X.detach().cpu().to(_F32) + offset) + noise.cpu().to(_F32) * noise_std
+        xd = _dev(x)
+        m = _lib.make_model(bin_boundaries, noise_std, offset, log_model)
+        Y = torch.empty(xd.shape, dtype=torch.int64, device=xd.device)
+        _lib.call("qsc_bin_codes", _lib.ptr(xd), xd.numel(), m, _lib.ptr(Y), _lib.stream())
+        return Y.to(out_dev)
     Xd = _dev(X.to(_F32))
     nd = _dev(noise.to(_F32))
     m = _lib.make_model(bin_boundaries, noise_std, offset if log_model else 0.0, log_model)

@@ -40,8 +40,9 @@ __global__ void __launch_bounds__(kBlock) quantize_kernel(const float* __restric
        i += (int64_t)gridDim.x * blockDim.x) {
     float base = X[i];
     if (log_model) base = logf(__fadd_rn(base, offset));
-    // X + randn*std: two separately rounded fp32 ops, exactly as the torch expression
-    const float x = __fadd_rn(base, __fmul_rn(noise[i], sigma));
+    // X + randn*std: two separately rounded fp32 ops, exactly as the torch expression; no
+    // noise (qsc_bin_codes): X already is the noisy observation
+    const float x = noise ? __fadd_rn(base, __fmul_rn(noise[i], sigma)) : base;
     int64_t y = 0;
     // later bins overwrite earlier ones, as the reference's loop of masked assignments does
     for (int c = 1; c <= nb - 2; ++c) {
@@ -416,6 +417,19 @@ QSC_API int qsc_quantize(const float* X, const float* noise, int64_t n, const qs
   hipLaunchKernelGGL(quantize_kernel, dim3(grid_for(n, 4, 8192)), dim3(kBlock), 0,
                      STREAM(stream), X, noise, n, B, m->nbounds, (float)m->sigma,
                      (float)m->offset, m->log_model, Y);
+  QSC_CHECK_LAUNCH();
+  return QSC_OK;
+}
+
+QSC_API int qsc_bin_codes(const float* x, int64_t n, const qsc_model* m, int64_t* Y,
+                          void* stream) {
+  if (!model_ok(m) || n < 0 || (n > 0 && (!x || !Y))) return QSC_EINVAL;
+  if (n == 0) return QSC_OK;
+  Bounds B;
+  for (int i = 0; i < m->nbounds; ++i) B.b[i] = m->bounds[i];
+  hipLaunchKernelGGL(quantize_kernel, dim3(grid_for(n, 4, 8192)), dim3(kBlock), 0,
+                     STREAM(stream), x, (const float*)nullptr, n, B, m->nbounds, 0.0f, 0.0f, 0,
+                     Y);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }

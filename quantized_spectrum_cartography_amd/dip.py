@@ -14,6 +14,7 @@ import torch
 from .nets import DecoderDip, SizedDecoderDip
 from .obs import Observations
 from .qmc import _solve_generator
+from .utils import LOG_OFFSET_7_ADJUSTED as LOG_OFFSET
 
 
 def make_decoder(I, J, zdim=256, seed=0):
@@ -30,11 +31,19 @@ def solve(Y, Wx, bin_boundaries, noise_std, R, offset=None, log_model=True, deco
           Z_init=None, C_init=None, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
           max_iter=500, optimize="weights", T_true=None, nmse_every=0, obs=None, tile=None,
           seed=0, callback=None):
-    """DIP-regularised alternating probit MLE (config 5: log model + DIP prior on S)."""
+    """DIP-regularised alternating probit MLE (config 5: log model + DIP prior on S).
+
+    `offset` defaults to the reference log model's LOG_OFFSET_7_ADJUSTED
+    (qmc/quantization_model_log.py:7, 9): with the zero C_init the first C-pass sees
+    T_hat = 0, and log(0 + offset) must stay finite."""
+    if log_model:
+        offset = LOG_OFFSET if offset is None else float(offset)
+        if not offset > 0.0:
+            raise ValueError("the log model needs offset > 0 (log(T_hat + offset) at T_hat = 0)")
     K = Y.shape[0]
     I, J = Y.shape[-2], Y.shape[-1]
     if obs is None:
-        obs = Observations(Y, Wx, bin_boundaries, noise_std, offset=offset or 0.0,
+        obs = Observations(Y, Wx, bin_boundaries, noise_std, offset=offset if log_model else 0.0,
                            log_model=log_model, tile=tile, R_hint=R)
     dev = obs.device
     if decoder is None:

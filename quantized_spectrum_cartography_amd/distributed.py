@@ -30,6 +30,7 @@ import torch
 
 from . import _lib
 from ._model import _dev
+from .qmc import issue_iterations, graph_for, run_iterations
 
 
 def kslab_bounds(K, world, rank):
@@ -49,68 +50,6 @@ def kslab_observations(Y_local, Wx_local, bin_boundaries, noise_std, dist, offse
         return cnt
     return Observations(Y_local, Wx_local, bin_boundaries, noise_std, offset=offset,
                         log_model=log_model, tile=tile, R_hint=R_hint, count_hook=hook)
-
-
-def _capture(solver, iters, body=None):
-    """Capture `iters` iterations (kernels + RCCL collectives) in one hipGraph; None if the
-    backend refuses capture (the solver then runs eagerly)."""
-    body = body or solver.iteration
-    try:
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                for _ in range(iters):
-                    body()
-        torch.cuda.current_stream().wait_stream(s)
-        return g
-    except Exception:  # pragma: no cover - depends on the RCCL build
-        torch.cuda.synchronize()
-        return None
-
-
-def _run_fused(solver, n, use_graph):
-    """C-step, then (S-step i + C-pass i+1 in one launch, the C finish / exchange) x (n-1), then
-    the last S-step: the kernel sequence of n plain iterations (FreeSSolver.run)."""
-    solver.c_step()
-    m = n - 1
-    if use_graph and torch.cuda.is_available() and solver.S.is_cuda:
-        if solver._fgraph is None and not solver._graph_failed:
-            gi = 1 if m < 8 else 8
-            g = _capture(solver, gi, solver.fused_body)
-            if g is None:
-                solver._graph_failed = True
-            else:
-                solver._fgraph, solver._fgraph_iters = g, gi
-        if solver._fgraph is not None:
-            k = m // solver._fgraph_iters
-            for _ in range(k):
-                solver._fgraph.replay()
-            m -= k * solver._fgraph_iters
-    for _ in range(m):
-        solver.fused_body()
-    solver.s_step()
-
-
-def _run(solver, n, use_graph):
-    if getattr(solver, "fuse", False) and n >= 2:
-        return _run_fused(solver, n, use_graph)
-    if use_graph and torch.cuda.is_available() and solver.S.is_cuda:
-        if solver._graph is None and not solver._graph_failed:
-            gi = 1 if n < 8 else 8
-            g = _capture(solver, gi)
-            if g is None:
-                solver._graph_failed = True
-            else:
-                solver._graph, solver._graph_iters = g, gi  # capture executes nothing
-        if solver._graph is not None:
-            k = n // solver._graph_iters
-            for _ in range(k):
-                solver._graph.replay()
-            n -= k * solver._graph_iters
-    for _ in range(n):
-        solver.iteration()
 
 
 class IJSlabSolver:
@@ -137,11 +76,11 @@ class IJSlabSolver:
         self.adam_s = _lib.make_adam(lr_s, betas, eps, project_nonneg=False)
         self.lambda_c, self.lambda_s = float(lambda_c), float(lambda_s)
         self.engine.init_state(self.S)
-        self._graph, self._graph_iters, self._graph_failed = None, 0, False
         # S-step + next C-pass in one launch (qsc_scpass), as FreeSSolver
         sup = getattr(self.engine, "scpass_supported", None)
         self.fuse = bool(fuse) and sup is not None and bool(sup())
-        self._fgraph, self._fgraph_iters = None, 0
+        self._graphs = {}
+        self.graph_tolerant, self.graph_error = True, None  # see qmc._capture
 
     def fused_body(self):
         """S-step i + C-pass i+1 (one launch), then C-step i+1's exchange and update."""
@@ -167,8 +106,14 @@ class IJSlabSolver:
         self.c_step()
         self.s_step()
 
+    def issue(self, n):
+        issue_iterations(self, n)
+
+    def prepare(self, n):
+        graph_for(self, n)
+
     def run(self, n, use_graph=False):
-        _run(self, n, use_graph)
+        run_iterations(self, n, use_graph)
 
     def state(self):
         return self.engine.read_state()
@@ -221,7 +166,8 @@ class KSlabSolver:
         self.adam_s = _lib.make_adam(lr_s, betas, eps, project_nonneg=False)
         self.lambda_c, self.lambda_s = float(lambda_c), float(lambda_s)
         self.engine.init_state(self.S)
-        self._graph, self._graph_iters, self._graph_failed = None, 0, False
+        self._graphs = {}
+        self.graph_tolerant, self.graph_error = True, None  # see qmc._capture
 
     def c_step(self):
         e = self.engine
@@ -241,8 +187,14 @@ class KSlabSolver:
         self.c_step()
         self.s_step()
 
+    def issue(self, n):
+        issue_iterations(self, n)
+
+    def prepare(self, n):
+        graph_for(self, n)
+
     def run(self, n, use_graph=False):
-        _run(self, n, use_graph)
+        run_iterations(self, n, use_graph)
 
     def state(self):
         return self.engine.read_state()

@@ -14,6 +14,7 @@ loop at :559-645); qmc/qmc.py is only its import preamble.  Per outer iteration 
     reference's GAN path, Z optimised, network frozen: :547-550).
 """
 import math
+import warnings
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -23,6 +24,7 @@ from . import _lib
 from ._model import _dev, map_nmse
 from .fused import PassEngine
 from .obs import Observations
+from .utils import LOG_OFFSET_7_ADJUSTED as LOG_OFFSET
 
 
 @dataclass
@@ -34,6 +36,71 @@ class SolveResult:
     nmse: List[float] = field(default_factory=list)  # map NMSE after each tracked iteration
     Z: Optional[torch.Tensor] = None
     iters: int = 0
+    fused: bool = False                 # S-step + next C-pass ran as one launch (qsc_scpass)
+
+
+# Longest run captured as one hipGraph; longer runs replay several (results are identical:
+# run(a) then run(b) equals run(a + b) bit for bit, tests/test_gpu_fused.py).
+GRAPH_MAX_ITERS = 1024
+
+
+def issue_iterations(solver, n):
+    """Kernel sequence of n outer iterations of a solver with c_step / s_step / iteration and,
+    when `solver.fuse`, fused_body (S-step i + C-pass i+1 in one launch, then C-step i+1's
+    finish): c_step, fused_body x (n-1), s_step -- two launches per iteration."""
+    if getattr(solver, "fuse", False) and n >= 2:
+        solver.c_step()
+        for _ in range(n - 1):
+            solver.fused_body()
+        solver.s_step()
+    else:
+        for _ in range(n):
+            solver.iteration()
+
+
+def _capture(solver, n, tolerant):
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    try:
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                issue_iterations(solver, n)
+    except RuntimeError as e:
+        if not tolerant:
+            raise
+        # sharded solvers: an RCCL build whose collectives cannot be captured (reported)
+        torch.cuda.synchronize()
+        solver.graph_error = "%s: %s" % (type(e).__name__, e)
+        warnings.warn("hipGraph capture failed; running eagerly (%s)" % solver.graph_error,
+                      RuntimeWarning)
+        return None
+    torch.cuda.current_stream().wait_stream(s)
+    return g
+
+
+def graph_for(solver, n):
+    """The hipGraph of the exact kernel sequence of run(n) (captured once per n)."""
+    graphs = solver.__dict__.setdefault("_graphs", {})
+    if n not in graphs:
+        graphs[n] = _capture(solver, n, getattr(solver, "graph_tolerant", False))
+    return graphs[n]
+
+
+def run_iterations(solver, n, use_graph):
+    """run(n): eager, or as replays of whole-run hipGraphs (one replay when n <= 1024), so the
+    device work of a timed run(n) does not depend on how earlier runs were split."""
+    if not (use_graph and torch.cuda.is_available() and solver.S.is_cuda):
+        issue_iterations(solver, n)
+        return
+    while n > 0:
+        m = min(n, GRAPH_MAX_ITERS)
+        g = graph_for(solver, m)
+        if g is None:
+            issue_iterations(solver, m)
+        else:
+            g.replay()
+        n -= m
 
 
 class FreeSSolver:
@@ -43,8 +110,8 @@ class FreeSSolver:
     An iteration is cpass, cfinish (C-step) then spass (S-step).  With `fuse` (default where
     qsc_scpass_supported) `run(n)` issues the same kernel sequence with each S-step and the
     following C-pass in one launch: cpass, cfinish, (scpass, cfinish) x (n-1), spass -- two
-    launches per iteration.  With `use_graph` the repeated body is captured once in a hipGraph
-    (torch.cuda.CUDAGraph) and replayed.
+    launches per iteration.  With `use_graph` the whole sequence of run(n) is captured once per
+    n in a hipGraph (torch.cuda.CUDAGraph) and replayed; `prepare(n)` captures it ahead.
     """
 
     def __init__(self, obs, S_init, C_init, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
@@ -61,11 +128,8 @@ class FreeSSolver:
         self.adam_s = _lib.make_adam(lr_s, betas, eps, project_nonneg=False)
         self.lambda_c, self.lambda_s = float(lambda_c), float(lambda_s)
         self.engine.init_state(self.S)
-        self._graph = None
-        self._graph_iters = 0
         self.fuse = bool(fuse) and self.engine.scpass_supported()
-        self._fgraph = None
-        self._fgraph_iters = 0
+        self._graphs = {}
 
     # one outer iteration = C grad-step + S grad-step
     def c_step(self):
@@ -87,55 +151,17 @@ class FreeSSolver:
         e.scpass(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s)
         e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)
 
-    def _capture_fused(self, iters):
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                for _ in range(iters):
-                    self.fused_body()
-        torch.cuda.current_stream().wait_stream(s)
-        self._fgraph, self._fgraph_iters = g, iters
+    def issue(self, n):
+        """Enqueue the kernel sequence of n outer iterations (no host sync)."""
+        issue_iterations(self, n)
 
-    def capture(self, iters=1):
-        """Capture `iters` iterations into one graph (replayed by run)."""
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                for _ in range(iters):
-                    self.iteration()
-        torch.cuda.current_stream().wait_stream(s)
-        self._graph, self._graph_iters = g, iters
+    def prepare(self, n):
+        """Capture the kernel sequence of run(n) in a hipGraph now (capture executes nothing),
+        so that a later run(n, use_graph=True) is exactly one graph replay."""
+        graph_for(self, n)
 
     def run(self, n, use_graph=False):
-        if self.fuse and n >= 2:
-            self.c_step()
-            m = n - 1
-            if use_graph:
-                if self._fgraph is None:
-                    self._capture_fused(1 if m < 8 else 8)
-                k = m // self._fgraph_iters
-                for _ in range(k):
-                    self._fgraph.replay()
-                m -= k * self._fgraph_iters
-            for _ in range(m):
-                self.fused_body()
-            self.s_step()
-            return
-        if use_graph:
-            if self._graph is None:
-                self.capture(1 if n < 8 else 8)
-            k = n // self._graph_iters
-            for _ in range(k):
-                self._graph.replay()
-            for _ in range(n - k * self._graph_iters):
-                self.iteration()
-        else:
-            for _ in range(n):
-                self.iteration()
+        run_iterations(self, n, use_graph)
 
     # ---- results --------------------------------------------------------------------------
     def state(self):
@@ -175,6 +201,11 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
     get_quantized_obs_from_ordinal); the cost history then holds that criterion.
     Returns a SolveResult with S (R,1,I,J) and C (R,K) on the GPU.
     """
+    if log_model and obs is None:
+        # the reference log model's default offset (qmc/quantization_model_log.py:7, 9)
+        offset = LOG_OFFSET if offset is None else float(offset)
+        if not offset > 0.0:
+            raise ValueError("the log model needs offset > 0 (log(T_hat + offset) at T_hat = 0)")
     K = Y.shape[0]
     I, J = Y.shape[-2], Y.shape[-1]
     if R is None:
@@ -203,7 +234,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
                 callback(done, sol)
         costs_c, costs_s = sol.history()
         return SolveResult(S=sol.S_pixels(), C=sol.C.clone(), costs_c=costs_c, costs_s=costs_s,
-                           nmse=nmse, iters=max_iter)
+                           nmse=nmse, iters=max_iter, fused=sol.fuse)
     return _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c, lr_s,
                             max_iter, betas, eps, project_c, restart, restart_samples, T_true,
                             nmse_every, callback)

@@ -106,6 +106,34 @@ def ijslab_onebit_problem(I, J, K, R, rank, world, dist=None, f=0.1, seed=20260,
                 log_model=False, offset=0.0, thr=thr, T_true=T)
 
 
+def split_problem(prob, rank, world, shard):
+    """This rank's shard of ONE global problem (strong scaling: the map is fixed, N ranks share
+    it).  shard="ijslab": rows [i0, i1) of the I axis (pixels), C replicated; shard="kslab":
+    frequency bins [k0, k1), S replicated.  Shards are views/slices of the global tensors, so
+    the union over ranks is the global problem exactly (tests/test_distributed_gloo.py)."""
+    from .distributed import kslab_bounds
+    out = dict(prob)
+    if shard == "ijslab":
+        I = prob["Y"].shape[-2]
+        i0, i1 = kslab_bounds(I, world, rank)
+        for key in ("S_true", "S0", "Y", "Wx", "T_true"):
+            if key in prob:
+                out[key] = prob[key][..., i0:i1, :].contiguous()
+        out["bounds"] = (i0, i1)
+    elif shard == "kslab":
+        K = prob["Y"].shape[0]
+        k0, k1 = kslab_bounds(K, world, rank)
+        for key in ("Y", "Wx", "T_true"):
+            if key in prob:
+                out[key] = prob[key][k0:k1].contiguous()
+        for key in ("C_true", "C0"):
+            out[key] = prob[key][:, k0:k1].contiguous()
+        out["bounds"] = (k0, k1)
+    else:
+        raise ValueError("shard must be 'ijslab' or 'kslab'")
+    return out
+
+
 CONFIGS = {
     # name: (I, J, K, R)   BASELINE.json configs
     "c2": (256, 256, 64, 4),

@@ -92,3 +92,26 @@ def test_host_constants_match_header():
     assert int(defs["QSC_MAX_BOUNDS"]) == _lib.QSC_MAX_BOUNDS
     assert int(defs["QSC_EINVAL"]) == _lib.QSC_EINVAL
     assert int(defs["QSC_UNOBSERVED"], 0) == _lib.UNOBSERVED
+
+
+def _c_sizeof_model():
+    src = '#include <stdio.h>\n#include "qsc.h"\nint main(void){printf("%zu %zu\\n", ' \
+          'sizeof(qsc_model), offsetof(qsc_model, loss));return 0;}\n'
+    d = tempfile.mkdtemp()
+    c, exe = os.path.join(d, "m.c"), os.path.join(d, "m")
+    open(c, "w").write("#include <stddef.h>\n" + src)
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+    return [int(x) for x in subprocess.check_output([exe]).split()]
+
+
+def test_integration_stub_struct_matches_c():
+    """The reference-side ctypes stub documented in INTEGRATION.md section 3 declares the same
+    qsc_model as the C header: exec the snippet's struct definition and compare sizes."""
+    import re
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    struct_src = re.search(r"(class _Model\(ctypes\.Structure\):.*?\]\n)", text, re.S).group(1)
+    ns = {"ctypes": ctypes}
+    exec(struct_src, ns)
+    size, loss_off = _c_sizeof_model()
+    assert ctypes.sizeof(ns["_Model"]) == size
+    assert ns["_Model"].loss.offset == loss_off

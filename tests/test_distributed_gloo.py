@@ -271,3 +271,60 @@ def test_ijslab_fused_sequence_equals_plain():
         out.append((sol.S.clone(), sol.C.clone(), eng.calls.count("scpass")))
     assert out[0][2] == ITERS - 1 and out[1][2] == 0
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
+def _global_problem_cpu(I_=12, J_=10, K_=16, R_=3, seed=5):
+    """A global problem dict with the keys synthetic.onebit_problem returns (CPU tensors)."""
+    g = torch.Generator().manual_seed(seed)
+    S_true = torch.rand(R_, 1, I_, J_, generator=g)
+    C_true = torch.rand(R_, K_, generator=g)
+    T_true = ro.get_tensor(S_true, C_true)
+    return dict(S_true=S_true, C_true=C_true, T_true=T_true,
+                Y=(T_true > T_true.median()).long().unsqueeze(1),
+                Wx=torch.bernoulli(torch.full((K_, 1, I_, J_), 0.3), generator=g),
+                S0=0.5 * torch.rand(R_, 1, I_, J_, generator=g),
+                C0=0.5 * torch.rand(R_, K_, generator=g),
+                b=torch.tensor([0.0, float(T_true.median()), float(T_true.max())]),
+                sigma=0.1, log_model=False, offset=0.0)
+
+
+def _split_worker(rank, world, port, out_path):
+    """Each rank takes its strong-scaling shard of the same global problem (bench.py
+    --scaling strong); the shards are all-gathered over gloo and must reassemble it."""
+    from quantized_spectrum_cartography_amd.synthetic import split_problem
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        glob = _global_problem_cpu()
+        ok = {}
+        for shard, axis_of in (("ijslab", dict(S_true=-2, S0=-2, Y=-2, Wx=-2, T_true=-2)),
+                               ("kslab", dict(Y=0, Wx=0, T_true=0, C_true=1, C0=1))):
+            sh = split_problem(glob, rank, world, shard)
+            for key, ax in axis_of.items():
+                parts = [torch.empty_like(sh[key]) for _ in range(world)]
+                dist.all_gather(parts, sh[key].contiguous())
+                ok["%s_%s" % (shard, key)] = bool(torch.equal(torch.cat(parts, dim=ax), glob[key]))
+            # the replicated blocks are the global ones
+            rep = ("C_true", "C0") if shard == "ijslab" else ("S_true", "S0")
+            for key in rep:
+                ok["%s_%s_replicated" % (shard, key)] = bool(torch.equal(sh[key], glob[key]))
+        np.savez(out_path + ".r%d" % rank, names=np.array(sorted(ok)),
+                 vals=np.array([ok[k] for k in sorted(ok)]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_strong_split_union_is_global_problem(tmp_path):
+    out = str(tmp_path / "split")
+    mp.start_processes(_split_worker, args=(2, _free_port(), out), nprocs=2, join=True,
+                       start_method="spawn")
+    for r in range(2):
+        d = np.load(out + ".r%d.npz" % r)
+        bad = [str(n) for n, v in zip(d["names"], d["vals"]) if not v]
+        assert not bad, bad
+    # uneven splits (C4 at N = 3, say) cover every row / bin exactly once
+    from quantized_spectrum_cartography_amd.synthetic import split_problem
+    glob = _global_problem_cpu(I_=13, K_=17)
+    for shard, ax in (("ijslab", -2), ("kslab", 0)):
+        parts = [split_problem(glob, r, 3, shard)["Y"] for r in range(3)]
+        assert torch.equal(torch.cat(parts, dim=ax), glob["Y"])

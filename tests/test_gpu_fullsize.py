@@ -1,0 +1,200 @@
+"""GPU parity at the BASELINE.json workloads themselves (configs C2-C5), not just small shapes.
+
+Each config runs through the fused HIP path and is checked against the fp64 closed-form oracle
+(oracle/explicit.py, evaluated at the observed entries only so that C3/C4 finish in seconds;
+itself pinned to the reference's autograd and goldens, tests/test_oracle_*.py):
+  * one pass: NLL, dS, dC at (S0, C0) vs explicit.nll_grad_obs             rel 1e-5
+  * 3 outer iterations of the alternating solver vs explicit.explicit_solve  rel Frobenius 1e-5
+    (the north_star tolerance on recovered S, C), costs rel 1e-5
+Reference anchors: qmc/qmc.ipynb :559-645 (loop, per-entry mask :493, likelihood :568-575),
+backup/notebooks/onebit_lowrank.ipynb :1230-1291 (free S).
+Configs: C2 256x256x64 R=4; C3 512x512x256 R=8 (the metric's config, fused scpass path);
+C4 one K-slab shard 512x512x128 R=16 of the 8-GPU 512x512x1024 problem through KSlabSolver
+(world 1, RCCL); C5 256x256x64 R=4 log model, 4 log bins, sigma 5, offset 1e-10, generated
+map, + the DIP path's fused dS at S = decoder(Z).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_fro
+from oracle import explicit
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5  # north_star: within 1e-5 relative (fp32)
+
+
+def _onebit(cfg, seed):
+    from quantized_spectrum_cartography_amd import synthetic
+    I, J, K, R = synthetic.CONFIGS[cfg]
+    return synthetic.onebit_problem(I, J, K, R, f=0.1, seed=seed), (I, J, K, R)
+
+
+def _np(t, shape=None):
+    a = t.detach().cpu().numpy()
+    return a.reshape(shape) if shape is not None else a
+
+
+def _pass_check(prob, dims, log_model=False, offset=0.0):
+    from quantized_spectrum_cartography_amd import fused
+    from quantized_spectrum_cartography_amd.obs import Observations
+    I, J, K, R = dims
+    P = I * J
+    obs = Observations(prob["Y"], prob["Wx"], prob["b"], prob["sigma"], offset=offset,
+                       log_model=log_model, R_hint=R)
+    S = prob["S0"].cuda().requires_grad_(True)
+    C = prob["C0"].cuda().requires_grad_(True)
+    nll = fused.ProbitNLL.apply(S, C, obs)
+    nll.backward()
+    ob = explicit.observed(_np(prob["Y"], (K, P)), _np(prob["Wx"], (K, P)))
+    assert ob[0].shape[0] == obs.nnz
+    rn, rdS, rdC = explicit.nll_grad_obs(_np(prob["S0"], (R, P)), _np(prob["C0"]), ob,
+                                         _np(prob["b"]), prob["sigma"], offset, log_model)
+    assert np.isfinite(rn)
+    assert abs(nll.item() - rn) / abs(rn) < TOL
+    assert rel_fro(_np(S.grad, (R, P)), rdS) < TOL
+    assert rel_fro(_np(C.grad), rdC) < TOL
+    return ob
+
+
+def _solver_check(prob, dims, ob, iters=3, log_model=False, offset=0.0, expect_fused=None):
+    from quantized_spectrum_cartography_amd import qmc
+    I, J, K, R = dims
+    P = I * J
+    res = qmc.solve(prob["Y"], prob["Wx"], prob["b"], prob["sigma"], S_init=prob["S0"],
+                    C_init=prob["C0"], max_iter=iters, log_model=log_model,
+                    offset=offset if log_model else None, use_graph=True)
+    if expect_fused is not None:
+        assert res.fused == expect_fused
+    S, C, cc, cs = explicit.explicit_solve(_np(prob["S0"], (R, P)), _np(prob["C0"]), ob,
+                                           _np(prob["b"]), prob["sigma"], offset, log_model,
+                                           n_iter=iters)
+    assert rel_fro(_np(res.S, (R, P)), S) < TOL
+    assert rel_fro(_np(res.C), C) < TOL
+    assert np.allclose(res.costs_c, cc, rtol=TOL) and np.allclose(res.costs_s, cs, rtol=TOL)
+
+
+@pytest.mark.parametrize("cfg,seed,fused", [("c2", 20262, False), ("c3", 20263, True)])
+def test_onebit_config_pass_and_solver(cfg, seed, fused):
+    """C2 / C3 (BASELINE.md section 3 recipe, the bench's own inputs for C3)."""
+    prob, dims = _onebit(cfg, seed)
+    ob = _pass_check(prob, dims)
+    _solver_check(prob, dims, ob, expect_fused=fused)
+
+
+def _c5_problem(seed=5):
+    from quantized_spectrum_cartography_amd import maps
+    from quantized_spectrum_cartography_amd import quantization_model_log as qml
+    from quantized_spectrum_cartography_amd.utils import (LOG_OFFSET_4,
+                                                          QUANTIZATION_BOUNDARIES_4_BINS_LOG)
+    K, R, I = 64, 4, 256
+    m = maps.generate_map(K, R, shadow_sigma=5.0, Xc=50.0, I=I, J=I, seed=seed)
+    g = torch.Generator().manual_seed(seed)
+    noise = torch.randn((K, I, I), generator=g)
+    b = torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG)
+    Y = qml.quantize(m["T"].cpu(), 5.0, b, offset=LOG_OFFSET_4, noise=noise).unsqueeze(1)
+    Wx = torch.bernoulli(torch.full((K, 1, I, I), 0.1), generator=g)
+    S0 = 0.5 * torch.rand(R, 1, I, I, generator=g) / I
+    C0 = 0.5 * torch.rand(R, K, generator=g)
+    prob = dict(Y=Y, Wx=Wx, b=b, sigma=5.0, S0=S0, C0=C0, S_true=m["S"], T_true=m["T"])
+    return prob, (I, I, K, R), LOG_OFFSET_4
+
+
+def test_c5_log_model_pass_and_solver():
+    """C5: log model, 4 log bins, sigma = 5, offset LOG_OFFSET_4 (qmc/qmc.ipynb :510-537)."""
+    prob, dims, off = _c5_problem()
+    assert len(torch.unique(prob["Y"])) >= 3  # the generated map spans the log bins
+    ob = _pass_check(prob, dims, log_model=True, offset=off)
+    _solver_check(prob, dims, ob, log_model=True, offset=off)
+
+
+def test_c5_dip_fused_dS_isolated():
+    """The HIP part of the DIP path at C5: the fused S-pass dS at S = decoder(Z) (the gradient
+    dip.solve back-propagates through the decoder) vs the fp64 oracle, 1e-5."""
+    from quantized_spectrum_cartography_amd import dip, fused
+    from quantized_spectrum_cartography_amd.obs import Observations
+    prob, (I, J, K, R), off = _c5_problem(seed=6)
+    P = I * J
+    dec = dip.make_decoder(I, J, seed=3).cuda().eval()
+    Z = torch.randn((R, 256), generator=torch.Generator().manual_seed(4)).cuda()
+    with torch.no_grad():
+        S_dec = dec(Z).reshape(R, 1, I, J) * (1.0 / I)
+    obs = Observations(prob["Y"], prob["Wx"], prob["b"], 5.0, offset=off, log_model=True,
+                       R_hint=R)
+    S = S_dec.clone().requires_grad_(True)
+    C = prob["C0"].cuda()
+    nll = fused.ProbitNLL.apply(S, C, obs)
+    nll.backward()
+    ob = explicit.observed(_np(prob["Y"], (K, P)), _np(prob["Wx"], (K, P)))
+    rn, rdS, _ = explicit.nll_grad_obs(_np(S_dec, (R, P)), _np(C), ob, _np(prob["b"]), 5.0, off,
+                                       True)
+    assert abs(nll.item() - rn) / abs(rn) < TOL
+    assert rel_fro(_np(S.grad, (R, P)), rdS) < TOL
+
+
+def test_c5_dip_solve_defaults_finite():
+    """dip.solve with its defaults (offset = the reference log model's LOG_OFFSET, zero C
+    init): the first C-pass sees T_hat = 0 and must stay finite."""
+    from quantized_spectrum_cartography_amd import dip
+    from quantized_spectrum_cartography_amd.utils import QUANTIZATION_BOUNDARIES_4_BINS_LOG
+    prob, (I, J, K, R), _ = _c5_problem(seed=7)
+    b = torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG)
+    res = dip.solve(prob["Y"][:, :, :64, :64].contiguous(), prob["Wx"][:, :, :64, :64].contiguous(),
+                    b, 5.0, R, max_iter=3)
+    assert np.all(np.isfinite(res.costs_c)) and np.all(np.isfinite(res.costs_s))
+    with pytest.raises(ValueError):
+        dip.solve(prob["Y"][:, :, :64, :64], prob["Wx"][:, :, :64, :64], b, 5.0, R, offset=0.0,
+                  max_iter=1)
+
+
+@pytest.fixture(scope="module")
+def pg():
+    import torch.distributed as dist
+    if dist.is_initialized():
+        yield dist
+        return
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0,
+                            world_size=1, device_id=torch.device("cuda", 0))
+    yield dist
+    dist.destroy_process_group()
+
+
+def test_c4_kslab_shard_pass_and_solver(pg):
+    """C4 per-GPU shard: 512x512 pixels x K_loc = 128 of the 1024 bins, R = 16, through the
+    north-star K-slab solver (RCCL world 1, hipGraph) -- pass and 3 iterations vs the oracle."""
+    from quantized_spectrum_cartography_amd import fused, synthetic
+    from quantized_spectrum_cartography_amd.distributed import KSlabSolver, kslab_observations
+    I, J, K, R = 512, 512, 128, 16
+    P = I * J
+    prob = synthetic.kslab_onebit_problem(I, J, K, R, 0, 1, dist=None, f=0.1, seed=20264)
+    obs = kslab_observations(prob["Y"], prob["Wx"], prob["b"], prob["sigma"], pg, R_hint=R)
+    S = prob["S0"].cuda().requires_grad_(True)
+    C = prob["C0"].cuda().requires_grad_(True)
+    nll = fused.ProbitNLL.apply(S, C, obs)
+    nll.backward()
+    ob = explicit.observed(_np(prob["Y"], (K, P)), _np(prob["Wx"], (K, P)))
+    bb = _np(prob["b"])
+    rn, rdS, rdC = explicit.nll_grad_obs(_np(prob["S0"], (R, P)), _np(prob["C0"]), ob, bb,
+                                         prob["sigma"])
+    assert abs(nll.item() - rn) / abs(rn) < TOL
+    assert rel_fro(_np(S.grad, (R, P)), rdS) < TOL
+    assert rel_fro(_np(C.grad), rdC) < TOL
+    sol = KSlabSolver(obs, prob["S0"], prob["C0"], dist=pg, hist_cap=8)
+    sol.run(3, use_graph=True)
+    torch.cuda.synchronize()
+    assert sol.graph_error is None
+    Sx, Cx, cc, cs = explicit.explicit_solve(_np(prob["S0"], (R, P)), _np(prob["C0"]), ob, bb,
+                                             prob["sigma"], n_iter=3)
+    assert rel_fro(_np(sol.S_pixels(), (R, P)), Sx) < TOL
+    assert rel_fro(_np(sol.C), Cx) < TOL
+    hc, hs = sol.history()
+    assert np.allclose(hc, cc, rtol=TOL) and np.allclose(hs, cs, rtol=TOL)

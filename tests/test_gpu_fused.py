@@ -139,24 +139,28 @@ def test_solver_graph_replay_matches_eager():
     assert np.array_equal(a.C.cpu().numpy(), b.C.cpu().numpy())
 
 
-@pytest.mark.parametrize("seed,R,I,J,K,log_model,loss,nbins",
-                         [(41, 4, 64, 64, 64, False, "probit", 2),
-                          (42, 8, 96, 80, 256, False, "probit", 2),
-                          (43, 3, 50, 70, 130, False, "probit", 2),
-                          (44, 5, 64, 64, 64, False, "squared", 2),
-                          (46, 4, 64, 64, 64, True, "probit", 2),
-                          (47, 6, 40, 56, 100, False, "probit", 20),   # wide (uint32) entries
-                          (48, 1, 33, 31, 70, False, "probit", 2)])    # R = 1, ragged P, K
-def test_fused_spass_cpass_bitexact(seed, R, I, J, K, log_model, loss, nbins):
+# tiles chosen so that every case has >= 4 C-pass units per tile (qsc_scpass_supported), i.e.
+# the fused launch really runs (asserted through SolveResult.fused)
+@pytest.mark.parametrize("seed,R,I,J,K,log_model,loss,nbins,tile",
+                         [(41, 4, 64, 64, 64, False, "probit", 2, 512),
+                          (42, 8, 96, 80, 256, False, "probit", 2, None),
+                          (43, 3, 50, 70, 130, False, "probit", 2, 256),
+                          (44, 5, 64, 64, 64, False, "squared", 2, 512),
+                          (46, 4, 64, 64, 64, True, "probit", 2, 512),
+                          (47, 6, 40, 56, 100, False, "probit", 20, 256),  # wide (uint32) entries
+                          (48, 1, 33, 31, 70, False, "probit", 2, 256)])   # R = 1, ragged P, K
+def test_fused_spass_cpass_bitexact(seed, R, I, J, K, log_model, loss, nbins, tile):
     """qsc_scpass (S-step + next C-pass in one launch) reproduces spass + cpass bit for bit:
     S, C and the cost history after n iterations, eager and hipGraph."""
     from quantized_spectrum_cartography_amd import qmc
     d = _random_case(seed, R, I, J, K, nbins=nbins, log_model=log_model)
     kw = dict(S_init=d["S0"], C_init=d["C0"], max_iter=11, loss=loss, offset=d["offset"],
-              log_model=log_model)
+              log_model=log_model, tile=tile)
     a = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], fuse=False, **kw)
+    assert not a.fused
     for g in (False, True):
         b = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], fuse=True, use_graph=g, **kw)
+        assert b.fused, "the fused S-step + C-pass launch did not run"
         assert np.array_equal(a.S.cpu().numpy(), b.S.cpu().numpy())
         assert np.array_equal(a.C.cpu().numpy(), b.C.cpu().numpy())
         assert a.costs_c == b.costs_c and a.costs_s == b.costs_s
@@ -300,3 +304,67 @@ def test_squared_solver_vs_reference_golden(golden):
     assert rel_fro(rn.C.cpu().numpy(), g["C_it%d" % n]) < 1e-5
     assert np.allclose(rn.costs_c, g["costs_c"], rtol=1e-5)
     assert np.allclose(rn.costs_s, g["costs_s"], rtol=1e-5)
+
+
+def _underflow_case(observed_flip):
+    """A one-bit problem, all entries observed but (optionally) one, with one entry's code put
+    on the wrong side of a sharp threshold so that its probit P underflows to exactly 0 in fp32
+    (erf saturates: F(thr - t) == 1 in qmc/quantization_model.py:61 arithmetic)."""
+    g = torch.Generator().manual_seed(3)
+    R, I, J, K = 2, 8, 8, 16
+    S = torch.rand(R, 1, I, J, generator=g) + 0.05
+    C = torch.rand(R, K, generator=g) + 0.05
+    Tt = ro.get_tensor(S, C)
+    thr = float(Tt.median())
+    b = torch.tensor([0.0, thr, float(Tt.max())])
+    sigma = 0.002 * (float(Tt.max()) - float(Tt.min()))
+    Y = (Tt > thr).long()
+    k, i, j = (Tt == Tt.min()).nonzero()[0].tolist()  # far below the threshold: code 0 ...
+    Y[k, i, j] = 1                                      # ... observed as 1: P == 0
+    Wx = torch.ones(K, 1, I, J)
+    if not observed_flip:
+        Wx[k, 0, i, j] = 0.0
+    return S, C, Y.unsqueeze(1), Wx, b, sigma, (k, i * J + j)
+
+
+def _reference_cost_grads(S, C, Y, Wx, b, sigma):
+    Sr, Cr = S.clone().requires_grad_(True), C.clone().requires_grad_(True)
+    nll = ro.masked_nll(Sr, Cr, Y, Wx, b, sigma)
+    nll.backward()
+    return nll.item(), Sr.grad.reshape(S.shape[0], -1).numpy(), Cr.grad.numpy()
+
+
+def test_observed_p_underflow_matches_reference():
+    """Reference semantics (qmc/qmc.ipynb :572, dense -sum(Wx log P)): an OBSERVED entry with
+    P == 0 makes the cost +inf and the gradients of its pixel / frequency bin non-finite; the
+    fused passes give the same non-finite cost and the same non-finite gradient entries."""
+    from quantized_spectrum_cartography_amd import fused
+    S, C, Y, Wx, b, sigma, (k, p) = _underflow_case(True)
+    rc, rdS, rdC = _reference_cost_grads(S, C, Y, Wx, b, sigma)
+    assert rc == float("inf")
+    obs = _obs(Y, Wx, b, sigma, R=2)
+    Sg, Cg = S.cuda().requires_grad_(True), C.cuda().requires_grad_(True)
+    nll = fused.ProbitNLL.apply(Sg, Cg, obs)
+    nll.backward()
+    assert nll.item() == float("inf")
+    dS = Sg.grad.cpu().reshape(2, -1).numpy()
+    dC = Cg.grad.cpu().numpy()
+    assert np.array_equal(np.isfinite(dS), np.isfinite(rdS))
+    assert np.array_equal(np.isfinite(dC), np.isfinite(rdC))
+    assert not np.isfinite(dS[:, p]).any() and not np.isfinite(dC[:, k]).any()
+
+
+def test_unobserved_p_underflow_is_a_deliberate_deviation():
+    """the reference evaluates every entry and multiplies by Wx, so an
+    UNOBSERVED entry with P == 0 yields 0 * log 0 = NaN for the whole cost; the build packs
+    observed entries only, so its cost and gradients stay finite (the documented deviation)."""
+    from quantized_spectrum_cartography_amd import fused
+    S, C, Y, Wx, b, sigma, _ = _underflow_case(False)
+    rc, _, _ = _reference_cost_grads(S, C, Y, Wx, b, sigma)
+    assert np.isnan(rc)
+    obs = _obs(Y, Wx, b, sigma, R=2)
+    Sg, Cg = S.cuda().requires_grad_(True), C.cuda().requires_grad_(True)
+    nll = fused.ProbitNLL.apply(Sg, Cg, obs)
+    nll.backward()
+    assert np.isfinite(nll.item())
+    assert np.isfinite(Sg.grad.cpu().numpy()).all() and np.isfinite(Cg.grad.cpu().numpy()).all()
