@@ -188,8 +188,32 @@ __device__ __forceinline__ float erf_fast(float x) {
 struct Lik {
   float a, inv_a, kgrad, offset;
   float thr;      // b[1]: the single active edge of the saturated one-bit model
-  float thr_a;    // fp32(thr / a): the one-bit model's z offset in the scaled form
+  float thr_a;    // fp32(thr / a): the general linear kind's z offset in the scaled form
+  // one-bit kind (Mills-ratio form, lik_grad2): z is carried as z*sqrt(log2 e)
+  float ob_scale; // fp32(sqrt(log2 e) / a): the factor rows are pre-scaled by -ob_scale
+  float ob_thr;   // fp32(thr * sqrt(log2 e) / a)
+  float ob_kg;    // fp32(kgrad / kMillsK)
 };
+
+// one-bit Mills-ratio form.  With c = sqrt(log2 e) and u = c |z|, the probit tail
+// 0.5 erfc(|z|) = exp(-z^2) * 0.5 erfcx(|z|) is evaluated as
+//     T = exp2(log2(kMillsK) - (c z)^2) * N(u) / D(u)
+// where kMillsK N/D is a (3,4) rational fit of 0.5 erfcx(u / c) on u in [0, 3.95 c] (relative
+// error 2.9e-7 in fp32, i.e. ~2 ulp; D has no roots on u >= 0, N/D -> 1/u for large u), N, D
+// monic.  Fitted by a Lawson-weighted linear least-squares in float64 (tools/fit_mills.py).
+constexpr float kMillsLogK = -1.5623618665631935f;
+constexpr float kMillsN2 = 6.567472368922525f, kMillsN1 = 17.9604287105516f,
+                kMillsN0 = 22.97849985876764f;
+constexpr float kMillsD3 = 6.547683092308922f, kMillsD2 = 18.821234758060108f,
+                kMillsD1 = 26.78107767395228f, kMillsD0 = 15.560871041019581f;
+constexpr double kMillsK = 0.3385963046956732;
+// Tail probabilities below 2^-25 are returned as exactly 0: where the reference's fp32
+// 0.5 * (1 + erf(z)) (qmc/quantization_model.py:61) has saturated (it does for tails below
+// 1.5e-8 .. 4.5e-8 depending on the side), so an observed entry that far out gets the
+// reference's P == 0, log P = -inf and a non-finite gradient (tests/test_gpu_fused.py).
+constexpr float kMillsTsat = 2.98023223876953125e-8f;  // 2^-25
+// z of pad entries: deep on the P == 1 side (E == 0), so they add exactly 0 to NLL and gradient
+constexpr float kPadZ = 1.0e4f;
 
 inline Lik make_lik(const qsc_model* m) {
   const Probit p = make_probit(m);
@@ -200,6 +224,10 @@ inline Lik make_lik(const qsc_model* m) {
   l.offset = p.offset;
   l.thr = m->nbounds >= 2 ? m->bounds[1] : 0.0f;
   l.thr_a = (float)((double)l.thr / (double)l.a);
+  const double c = 1.2011224087864498;  // sqrt(log2 e)
+  l.ob_scale = (float)(c / (double)l.a);
+  l.ob_thr = (float)((double)l.thr * c / (double)l.a);
+  l.ob_kg = (float)((double)p.kgrad / kMillsK);
   return l;
 }
 
@@ -223,47 +251,6 @@ __device__ __forceinline__ float div_lik(float x, const Lik& c) {
 constexpr float kNegLog2e = -1.44269504088896340736f;
 constexpr float kLn2 = 0.69314718055994530942f;
 constexpr float kInvLn2 = 1.44269504088896340736f;
-
-// One observed entry: t = reconstruction value; returns log2 P (the caller scales the summed
-// NLL by ln 2 once) and g = d(-log P)/dt.  Branch-free; `edges` is only read by the general kind.
-template <int KIND, bool LOG>
-__device__ __forceinline__ void lik_grad(float t, int code, const float2* __restrict__ edges,
-                                         const Lik& c, float& log2P, float& g) {
-  if (KIND == LIK_SQUARED) {
-    float x = t, tinv = 1.0f;
-    if (LOG) {
-      const float tp = t + c.offset;
-      x = logf(tp);
-      tinv = __builtin_amdgcn_rcpf(tp);
-    }
-    const float r = x - edges[code].x;
-    g = 2.0f * r * tinv;
-    log2P = -(r * r) * kInvLn2;
-  } else if (KIND == LIK_ONEBIT) {
-    const float z = div_lik(c.thr - t, c);
-    const float F = 0.5f * (1.0f + erf_fast(z));
-    const bool c0 = (code == 0);
-    const float P = c0 ? F : 1.0f - F;
-    const float e = __builtin_amdgcn_exp2f(z * z * kNegLog2e) * c.kgrad;  // exp(-z^2) / (a sqrt(pi))
-    g = (c0 ? e : -e) * __builtin_amdgcn_rcpf(P);
-    log2P = __builtin_amdgcn_logf(P);
-  } else {
-    float x = t, tinv = 1.0f;
-    if (LOG) {
-      const float tp = t + c.offset;
-      x = logf(tp);
-      tinv = __builtin_amdgcn_rcpf(tp);
-    }
-    const float2 e2 = edges[code];
-    const float u = div_lik(e2.y - x, c);
-    const float w = div_lik(e2.x - x, c);
-    const float P = 0.5f * (1.0f + erf_fast(u)) - 0.5f * (1.0f + erf_fast(w));
-    const float d = (__builtin_amdgcn_exp2f(u * u * kNegLog2e) -
-                     __builtin_amdgcn_exp2f(w * w * kNegLog2e)) * c.kgrad;
-    g = d * __builtin_amdgcn_rcpf(P) * tinv;
-    log2P = __builtin_amdgcn_logf(P);
-  }
-}
 
 // ------------------------------------------------------------------------------------
 // Two-entry (packed) forms.  gfx950 issues a wave64 f32 VALU op every ~4 cycles whether it is
@@ -314,15 +301,26 @@ __device__ __forceinline__ f2v log2_2(f2v x) {
   return f2v{__builtin_amdgcn_logf(x.x), __builtin_amdgcn_logf(x.y)};
 }
 
-// lik_grad for two entries (t.x with code c0, t.y with code c1).
-// Linear model (one-bit and multi-bin): the caller passes t in the SCALED form t' = -t / a
-// (its register factor vector pre-multiplied by -1/a, so the dot product yields t' directly)
-// and, for the general kind, edges pre-divided by a: z = thr/a + t', u = hi/a + t',
-// w = lo/a + t' (one add instead of a subtract and a division per entry).  The log model takes
-// t itself (x = log(t + offset) needs it).
+// lik_grad for two entries (t.x with code c0, t.y with code c1); log2P and g of -log P.
+// Linear general kind: the caller passes t in the SCALED form t' = -t / a (its register factor
+// vector pre-multiplied by -1/a, so the dot product yields t' directly) and edges pre-divided by
+// a: u = hi/a + t', w = lo/a + t' (one add instead of a subtract and a division per entry).  The
+// log model takes t itself (x = log(t + offset) needs it).
+// One-bit kind (Mills-ratio form): the caller passes z' = c (thr - t) / a (c = sqrt(log2 e):
+// own factors pre-scaled by -Lik::ob_scale, the dot seeded with Lik::ob_thr), and pad flags:
+// pad entries are moved to z' = kPadZ (P == 1, g == 0, log2 P == 0) instead of being masked.
+//     T = 0.5 erfc(|z|) (0 below 2^-25),  P = T on the tail side (code 0: z < 0; code 1:
+//     z > 0) else 1 - T,  g = +-exp(-z^2) / (a sqrt(pi) P)  (+ for code 0, - for code 1)
+// The reference forms P = F(hi - x) - F(lo - x) with F = 0.5 (1 + erf) and the +-1e5 clamp
+// (qmc/quantization_model.py:32-38, :61): with one edge saturated that is F(z) for code 0 and
+// 1 - F(z) for code 1, the same probability; this form evaluates it without the cancellation
+// of 1 - F in the tail (the values agree to a few ulp where the reference is accurate, P well
+// away from 0) and without erf's two polynomial branches: one exp2, two rcp, one log2 and a
+// (3,4) rational per entry.  Codes: the one-bit kind reads code != 1 as code 0 (pads are 15).
 template <int KIND, bool LOG>
-__device__ __forceinline__ void lik_grad2(f2v t, int c0, int c1, const float2* __restrict__ edges,
-                                          const Lik& c, f2v& log2P, f2v& g) {
+__device__ __forceinline__ void lik_grad2(f2v t, int c0, int c1, bool pa, bool pb,
+                                          const float2* __restrict__ edges, const Lik& c,
+                                          f2v& log2P, f2v& g) {
   if (KIND == LIK_SQUARED) {
     // r = x - Obs; loss r^2 (returned as -r^2/ln2: the passes scale the summed log2 P by
     // ln 2); g = d(r^2)/dt = 2 r dx/dt.  t is unscaled for this kind.
@@ -337,14 +335,26 @@ __device__ __forceinline__ void lik_grad2(f2v t, int c0, int c1, const float2* _
     g = splat2(2.0f) * r * tinv;
     log2P = -(r * r) * splat2(kInvLn2);
   } else if (KIND == LIK_ONEBIT) {
-    const f2v z = splat2(c.thr_a) + t;
-    const f2v F = splat2(0.5f) * (splat2(1.0f) + erf_fast2(z));
-    const f2v Fc = splat2(1.0f) - F;
-    const bool z0 = (c0 == 0), z1 = (c1 == 0);
-    const f2v P = f2v{z0 ? F.x : Fc.x, z1 ? F.y : Fc.y};
-    const f2v e = exp2_2(z * z * splat2(kNegLog2e)) * splat2(c.kgrad);
-    const f2v rp = rcp2(P);
-    g = f2v{z0 ? e.x : -e.x, z1 ? e.y : -e.y} * rp;
+    f2v z = t;
+    if (pa) z.x = kPadZ;
+    if (pb) z.y = kPadZ;
+    const f2v u = f2v{__builtin_fabsf(z.x), __builtin_fabsf(z.y)};
+    const f2v E = exp2_2(fma2(-z, z, splat2(kMillsLogK)));  // kMillsK exp(-z^2)
+    f2v N = u + splat2(kMillsN2);
+    N = fma2(N, u, splat2(kMillsN1));
+    N = fma2(N, u, splat2(kMillsN0));
+    f2v D = u + splat2(kMillsD3);
+    D = fma2(D, u, splat2(kMillsD2));
+    D = fma2(D, u, splat2(kMillsD1));
+    D = fma2(D, u, splat2(kMillsD0));
+    const f2v T = (E * N) * rcp2(D);
+    const f2v Ts = f2v{T.x < kMillsTsat ? 0.0f : T.x, T.y < kMillsTsat ? 0.0f : T.y};
+    const f2v Q = splat2(1.0f) - Ts;
+    const bool z0 = (c0 != 1), z1 = (c1 != 1);
+    const bool ta = (z.x < 0.0f) == z0, tb = (z.y < 0.0f) == z1;
+    const f2v P = f2v{ta ? Ts.x : Q.x, tb ? Ts.y : Q.y};
+    const f2v gm = (E * splat2(c.ob_kg)) * rcp2(P);
+    g = f2v{z0 ? gm.x : -gm.x, z1 ? gm.y : -gm.y};
     log2P = log2_2(P);
   } else {
     const float2 e0 = edges[c0], e1 = edges[c1];
@@ -365,111 +375,6 @@ __device__ __forceinline__ void lik_grad2(f2v t, int c0, int c1, const float2* _
                   splat2(c.kgrad);
     g = d * rcp2(P) * tinv;
     log2P = log2_2(P);
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Four-entry forms: the same per-element operation sequence as lik_grad2 (bitwise the same
-// results) on 4-wide vectors, which the backend splits into two independent v_pk_* chains.
-// Interleaving the two chains fills the issue slot that a dependent packed op would otherwise
-// spend on an s_nop (packed-VALU read-after-write hazard) and doubles the ILP per wave.
-// ------------------------------------------------------------------------------------
-typedef float f4v __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ f4v fma4(f4v a, f4v b, f4v c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f4v splat4(float x) { return f4v{x, x, x, x}; }
-__device__ __forceinline__ f4v exp2_4(f4v x) {
-  return f4v{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y), __builtin_amdgcn_exp2f(x.z),
-             __builtin_amdgcn_exp2f(x.w)};
-}
-__device__ __forceinline__ f4v rcp4(f4v x) {
-  return f4v{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y), __builtin_amdgcn_rcpf(x.z),
-             __builtin_amdgcn_rcpf(x.w)};
-}
-__device__ __forceinline__ f4v log2_4(f4v x) {
-  return f4v{__builtin_amdgcn_logf(x.x), __builtin_amdgcn_logf(x.y), __builtin_amdgcn_logf(x.z),
-             __builtin_amdgcn_logf(x.w)};
-}
-__device__ __forceinline__ f4v sel4(bool c0, bool c1, bool c2, bool c3, f4v a, f4v b) {
-  return f4v{c0 ? a.x : b.x, c1 ? a.y : b.y, c2 ? a.z : b.z, c3 ? a.w : b.w};
-}
-
-__device__ __forceinline__ f4v erf_fast4(f4v x) {
-  const f4v ax = __builtin_elementwise_abs(x);
-  f4v p = fma4(ax, splat4(bits(0x378e98abu)), splat4(bits(0xb9c68948u)));
-  p = fma4(ax, p, splat4(bits(0x3b7cd369u)));
-  p = fma4(ax, p, splat4(bits(0xbcc618b2u)));
-  p = fma4(ax, p, splat4(bits(0x3dda74e4u)));
-  p = fma4(ax, p, splat4(bits(0x3f228afdu)));
-  p = fma4(ax, p, splat4(bits(0x3e03c728u)));
-  p = fma4(ax, p, ax);
-  const f4v pe = p * splat4(bits(0xbfb8aa3bu));
-  const f4v big = splat4(1.0f) - exp2_4(pe);
-  const f4v t = x * x;
-  f4v q = fma4(splat4(bits(0xba1345e1u)), t, splat4(bits(0x3ba10414u)));
-  q = fma4(t, q, splat4(bits(0xbcdac9b8u)));
-  q = fma4(t, q, splat4(bits(0x3de703beu)));
-  q = fma4(t, q, splat4(bits(0xbec09330u)));
-  q = fma4(t, q, splat4(bits(0x3e0375d0u)));
-  const f4v small = fma4(ax, q, ax);
-  return f4v{__builtin_copysignf(ax.x < 1.0f ? small.x : big.x, x.x),
-             __builtin_copysignf(ax.y < 1.0f ? small.y : big.y, x.y),
-             __builtin_copysignf(ax.z < 1.0f ? small.z : big.z, x.z),
-             __builtin_copysignf(ax.w < 1.0f ? small.w : big.w, x.w)};
-}
-
-__device__ __forceinline__ f4v div_lik4(f4v x, const Lik& c) {
-  const f4v ia = splat4(c.inv_a);
-  const f4v q = x * ia;
-  const f4v r = fma4(-q, splat4(c.a), x);
-  return fma4(r, ia, q);
-}
-
-// lik_grad2 on four entries (codes c[0..3]); same scaled-form convention
-template <int KIND, bool LOG>
-__device__ __forceinline__ void lik_grad4(f4v t, const int (&cd)[4],
-                                          const float2* __restrict__ edges, const Lik& c,
-                                          f4v& log2P, f4v& g) {
-  if (KIND == LIK_SQUARED) {
-    const float2 e0 = edges[cd[0]], e1 = edges[cd[1]], e2 = edges[cd[2]], e3 = edges[cd[3]];
-    f4v x = t, tinv = splat4(1.0f);
-    if (LOG) {
-      const f4v tp = t + splat4(c.offset);
-      x = f4v{logf(tp.x), logf(tp.y), logf(tp.z), logf(tp.w)};
-      tinv = rcp4(tp);
-    }
-    const f4v r = x - f4v{e0.x, e1.x, e2.x, e3.x};
-    g = splat4(2.0f) * r * tinv;
-    log2P = -(r * r) * splat4(kInvLn2);
-  } else if (KIND == LIK_ONEBIT) {
-    const f4v z = splat4(c.thr_a) + t;
-    const f4v F = splat4(0.5f) * (splat4(1.0f) + erf_fast4(z));
-    const f4v Fc = splat4(1.0f) - F;
-    const bool z0 = (cd[0] == 0), z1 = (cd[1] == 0), z2 = (cd[2] == 0), z3 = (cd[3] == 0);
-    const f4v P = sel4(z0, z1, z2, z3, F, Fc);
-    const f4v e = exp2_4(z * z * splat4(kNegLog2e)) * splat4(c.kgrad);
-    const f4v rp = rcp4(P);
-    g = sel4(z0, z1, z2, z3, e, -e) * rp;
-    log2P = log2_4(P);
-  } else {
-    const float2 e0 = edges[cd[0]], e1 = edges[cd[1]], e2 = edges[cd[2]], e3 = edges[cd[3]];
-    f4v u, w, tinv = splat4(1.0f);
-    if (LOG) {
-      const f4v tp = t + splat4(c.offset);
-      const f4v x = f4v{logf(tp.x), logf(tp.y), logf(tp.z), logf(tp.w)};
-      tinv = rcp4(tp);
-      u = div_lik4(f4v{e0.y, e1.y, e2.y, e3.y} - x, c);
-      w = div_lik4(f4v{e0.x, e1.x, e2.x, e3.x} - x, c);
-    } else {
-      u = f4v{e0.y, e1.y, e2.y, e3.y} + t;
-      w = f4v{e0.x, e1.x, e2.x, e3.x} + t;
-    }
-    const f4v P = splat4(0.5f) * (splat4(1.0f) + erf_fast4(u)) -
-                  splat4(0.5f) * (splat4(1.0f) + erf_fast4(w));
-    const f4v d = (exp2_4(u * u * splat4(kNegLog2e)) - exp2_4(w * w * splat4(kNegLog2e))) *
-                  splat4(c.kgrad);
-    g = d * rcp4(P) * tinv;
-    log2P = log2_4(P);
   }
 }
 

@@ -112,6 +112,27 @@ __device__ __forceinline__ float dot2(const f2v (&own)[RP / 2], const f2v (&o)[R
   return d.x + d.y;
 }
 
+// z0 + sum_r own[r] * o[r]: the one-bit kind's z' with its offset seeded into the first FMA
+template <int RP>
+__device__ __forceinline__ float dot2z(const f2v (&own)[RP / 2], const f2v (&o)[RP / 2], float z0) {
+  f2v d = fma2(own[0], o[0], f2v{z0, 0.0f});
+#pragma unroll
+  for (int j = 1; j < RP / 2; ++j) d = fma2(own[j], o[j], d);
+  // an opaque (empty) asm on the sum keeps it one v_add_f32: without it the backend turns the
+  // two entries' horizontal adds into three v_mov + a v_pk_add_f32
+  float r = d.x + d.y;
+  asm("" : "+v"(r));
+  return r;
+}
+
+// factor the register row is pre-multiplied by: linear kinds evaluate in a scaled form
+// (lik_grad2): -1/a (general), -sqrt(log2 e)/a (one-bit); the log model / squared loss use t
+template <int KIND, bool LOG>
+__device__ __forceinline__ float own_scale_of(const Lik& lk) {
+  if (LOG || KIND == LIK_SQUARED) return 1.0f;
+  return KIND == LIK_ONEBIT ? -lk.ob_scale : -lk.inv_a;
+}
+
 struct Scalars {
   float coef;  // lambda / ||x||  (0 when ||x|| == 0, as torch's norm backward)
   AdamScalars as;
@@ -119,46 +140,17 @@ struct Scalars {
 
 // Process one 4-entry chunk as two packed pairs: `own` is the lane's register vector (S of the
 // pixel or C of the frequency bin, r-pairs), `tab` the LDS table of the other factor indexed by
-// the entry's low bits.  Pad entries carry index 0 (a valid row) and code kPad; their gradient
-// and log-likelihood are masked.
+// the entry's low bits.  Pad entries carry index 0 (a valid row) and code kPad; the one-bit kind
+// moves them to z' = kPadZ where they contribute exactly 0, the other kinds mask them.  The NLL
+// is accumulated as a pair (summed by the caller).
 template <int RP, typename E, int KIND, bool LOG>
 __device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const f2v (&own)[RP / 2],
                                       const float* __restrict__ tab,
                                       const float2* __restrict__ edges, const Lik& lk,
-                                      f2v (&acc)[RP / 2], float& nll, bool valid = true) {
+                                      f2v (&acc)[RP / 2], f2v& nll, bool valid = true) {
   using T = Ent<E>;
   uint32_t e[4];
   T::unpack(v, e);
-#if QSC_CHUNK4
-  // all four entries at once: four gathers in flight, then the per-entry math as two
-  // interleaved packed chains (lik_grad4); sums in the same order as the pairwise form
-  {
-    int cd[4];
-    bool pd[4];
-    f2v o[4][RP / 2];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int cu = (int)(e[u] >> T::kBits);
-      pd[u] = (cu == T::kPad) || !valid;
-      cd[u] = pd[u] ? 0 : cu;
-      lds_row2<RP>(tab + (e[u] & T::kMask) * Pitch<RP>::v, o[u]);
-    }
-    const f4v t = f4v{dot2<RP>(own, o[0]), dot2<RP>(own, o[1]), dot2<RP>(own, o[2]),
-                      dot2<RP>(own, o[3])};
-    f4v log2P, g;
-    lik_grad4<KIND, LOG>(t, cd, edges, lk, log2P, g);
-    const float gu[4] = {pd[0] ? 0.0f : g.x, pd[1] ? 0.0f : g.y, pd[2] ? 0.0f : g.z,
-                         pd[3] ? 0.0f : g.w};
-    nll -= (pd[0] ? 0.0f : log2P.x) + (pd[1] ? 0.0f : log2P.y);
-    nll -= (pd[2] ? 0.0f : log2P.z) + (pd[3] ? 0.0f : log2P.w);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-#pragma unroll
-      for (int j = 0; j < RP / 2; ++j) acc[j] = fma2(splat2(gu[u]), o[u][j], acc[j]);
-    }
-    return;
-  }
-#endif
 #pragma unroll
   for (int u = 0; u < 4; u += 2) {
     const int ca = (int)(e[u] >> T::kBits), cb = (int)(e[u + 1] >> T::kBits);
@@ -174,16 +166,29 @@ __device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const f2v (&
     lds_row2<RP>(tab + (e[u] & T::kMask) * Pitch<RP>::v, oa);
     lds_row2<RP>(tab + (e[u + 1] & T::kMask) * Pitch<RP>::v, ob);
 #endif
-    const f2v t = f2v{dot2<RP>(own, oa), dot2<RP>(own, ob)};
+    f2v t;
+    if constexpr (KIND == LIK_ONEBIT)
+      t = f2v{dot2z<RP>(own, oa, lk.ob_thr), dot2z<RP>(own, ob, lk.ob_thr)};
+    else
+      t = f2v{dot2<RP>(own, oa), dot2<RP>(own, ob)};
     f2v log2P, g;
 #if QSC_DIAG_NOMATH  // diagnostic build: no likelihood arithmetic (bounds the VALU share)
     g = t * splat2(1e-3f);
     log2P = t;
 #else
-    lik_grad2<KIND, LOG>(t, pa ? 0 : ca, pb ? 0 : cb, edges, lk, log2P, g);
+    if constexpr (KIND == LIK_ONEBIT)
+      lik_grad2<KIND, LOG>(t, ca, cb, pa, pb, edges, lk, log2P, g);
+    else
+      lik_grad2<KIND, LOG>(t, pa ? 0 : ca, pb ? 0 : cb, pa, pb, edges, lk, log2P, g);
 #endif
-    const float ga = pa ? 0.0f : g.x, gb = pb ? 0.0f : g.y;
-    nll -= (pa ? 0.0f : log2P.x) + (pb ? 0.0f : log2P.y);  // log2 units: scaled by ln 2 later
+    float ga = g.x, gb = g.y;
+    if constexpr (KIND == LIK_ONEBIT) {
+      nll -= log2P;  // log2 units: scaled by ln 2 later
+    } else {
+      ga = pa ? 0.0f : ga;
+      gb = pb ? 0.0f : gb;
+      nll -= f2v{pa ? 0.0f : log2P.x, pb ? 0.0f : log2P.y};
+    }
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) acc[j] = fma2(splat2(ga), oa[j], acc[j]);
 #pragma unroll
@@ -218,7 +223,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
                                             const f2v (&own)[RP / 2],
                                             const float* __restrict__ tab,
                                             const float2* __restrict__ edges, const Lik& lk,
-                                            f2v (&acc)[RP / 2], float& nll) {
+                                            f2v (&acc)[RP / 2], f2v& nll) {
   using V4 = typename Ent<E>::V4;
   const int jlast = max(j1 - 1, 0);
   for (;;) {
@@ -249,7 +254,7 @@ __device__ __forceinline__ void walk_masked(const typename Ent<E>::V4* __restric
                                             const f2v (&own)[RP / 2],
                                             const float* __restrict__ tab,
                                             const float2* __restrict__ edges, const Lik& lk,
-                                            f2v (&acc)[RP / 2], float& nll) {
+                                            f2v (&acc)[RP / 2], f2v& nll) {
   using V4 = typename Ent<E>::V4;
   j1 = __builtin_amdgcn_readfirstlane(j1);
   ju = __builtin_amdgcn_readfirstlane(ju);
@@ -449,8 +454,8 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     float* __restrict__ part_nll, float* __restrict__ part_nsq, int* __restrict__ sched) {
   constexpr int CP = Pitch<RP>::v;
   constexpr int RH = RP / 2;  // row elements updated per lane (half row)
-  // linear models evaluate the entries in the scaled form t' = -t/a (lik_grad2)
-  const float own_scale = (LOG || KIND == LIK_SQUARED) ? 1.0f : -lk.inv_a;
+  // linear models evaluate the entries in a scaled form (lik_grad2)
+  const float own_scale = own_scale_of<KIND, LOG>(lk);
   // all LDS carved from the 16-B aligned dynamic region (no statics ahead of it)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   Scalars& sc = *reinterpret_cast<Scalars*>(smem);            // 32 B reserved
@@ -551,7 +556,7 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     f2v accp[RP / 2];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
-    float nll = 0.0f;
+    f2v nll = splat2(0.0f);
 #if QSC_SPASS_MASKED
     walk_masked<RP, E, KIND, LOG>(cur.src, QSC_SLICE, h, 0, cur.j1, 2, cur.buf, own, Cl, El, lk,
                                   accp, nll);
@@ -594,8 +599,8 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     } else {
       st_row<RH>(dS + row + h * RH, a);
     }
-    nll = wave_sum_dpp(nll) * kLn2;
-    if (lane == 0) part_nll[s] = nll;
+    const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
+    if (lane == 0) part_nll[s] = nll_w;
     STAMP(w, 4 + 3 * i);
     if (!more) break;
     cur.assign(nxt);
@@ -678,7 +683,7 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   STAMP(wg, 1);
 
   // 3. likelihood + gradient over the part lists
-  const float own_scale = (LOG || KIND == LIK_SQUARED) ? 1.0f : -lk.inv_a;  // scaled form t' = -t/a (lik_grad2)
+  const float own_scale = own_scale_of<KIND, LOG>(lk);  // scaled form (lik_grad2)
   f2v own[RP / 2];
 #pragma unroll
   for (int j = 0; j < RP / 2; ++j)
@@ -687,20 +692,20 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   f2v accp[RP / 2];
 #pragma unroll
   for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
-  float nll = 0.0f;
+  f2v nll = splat2(0.0f);
 #if QSC_CPASS_MASKED
   walk_masked<RP, E, KIND, LOG>(src, 64, j0, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
 #else
   walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
 #endif
   STAMP(wg, 2);
-  nll = wave_sum_dpp(nll) * kLn2;
+  const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
 #pragma unroll
   for (int j = 0; j < RP / 2; ++j) {
     if (2 * j < R) Pl[((size_t)part * R + 2 * j) * 64 + lane] = accp[j].x;
     if (2 * j + 1 < R) Pl[((size_t)part * R + 2 * j + 1) * 64 + lane] = accp[j].y;
   }
-  if (lane == 0) Nl[part] = nll;
+  if (lane == 0) Nl[part] = nll_w;
   __syncthreads();
   STAMP(wg, 3);
 
@@ -757,7 +762,7 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
   const int t = blockIdx.x;
   const int Kp = nks * 64;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const float own_scale = (LOG || KIND == LIK_SQUARED) ? 1.0f : -lk.inv_a;  // scaled form t' = -t/a (lik_grad2)
+  const float own_scale = own_scale_of<KIND, LOG>(lk);  // scaled form (lik_grad2)
   [[maybe_unused]] const int wg = blockIdx.x * (kCTBlock / 64) + w;  // (diagnostic stamps)
   STAMP(wg, 0);
   RSTAMP(wg, 28);
@@ -809,9 +814,9 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
     f2v accp[RP / 2];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
-    float nll = 0.0f;
+    f2v nll = splat2(0.0f);
     walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
-    nll = wave_sum_dpp(nll) * kLn2;
+    const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (NP == 1) {
       // the unit is the whole (tile, k-slice): its slab rows straight from registers
 #pragma unroll
@@ -819,14 +824,14 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
         if (2 * j < R) slab[((int64_t)t * R + 2 * j) * Kp + k] = accp[j].x;
         if (2 * j + 1 < R) slab[((int64_t)t * R + 2 * j + 1) * Kp + k] = accp[j].y;
       }
-      if (lane == 0) part_nll[wi] = nll;
+      if (lane == 0) part_nll[wi] = nll_w;
     } else {
 #pragma unroll
       for (int j = 0; j < RP / 2; ++j) {
         if (2 * j < R) Pl[((size_t)u * R + 2 * j) * 64 + lane] = accp[j].x;
         if (2 * j + 1 < R) Pl[((size_t)u * R + 2 * j + 1) * 64 + lane] = accp[j].y;
       }
-      if (lane == 0) Nl[u] = nll;
+      if (lane == 0) Nl[u] = nll_w;
     }
     if (u + NW < U) unit_begin(u + NW);
   }
@@ -907,7 +912,7 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int p = lane & (QSC_SLICE - 1), h = lane >> 5;
   const uint32_t hmask = 0u - (uint32_t)h;
-  const float own_scale = (LOG || KIND == LIK_SQUARED) ? 1.0f : -lk.inv_a;
+  const float own_scale = own_scale_of<KIND, LOG>(lk);
   const int nsl = PT / QSC_SLICE;  // slices per tile
   // this wave's n-th slice of the tile (local index) and its global slice
   auto local_of = [&](int n) { return n * NW + ((n & 1) ? (NW - 1 - w) : w); };
@@ -998,7 +1003,7 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
     f2v accp[RP / 2];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
-    float nll = 0.0f;
+    f2v nll = splat2(0.0f);
     walk_groups<RP, E, KIND, LOG>(cur.src, QSC_SLICE, h, cur.j1, 2, cur.buf, own, Cl, El, lk,
                                   accp, nll);
     float acc[RP];
@@ -1025,8 +1030,8 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
     st_row<RH>(Sl + (il * QSC_SLICE + p) * CP + h * RH, pv);  // the tile row, for the C-pass
     nsq = wave_sum_dpp(nsq);
     if (lane == 0) part_nsq_s[s] = nsq;
-    nll = wave_sum_dpp(nll) * kLn2;
-    if (lane == 0) part_nll_s[s] = nll;
+    const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
+    if (lane == 0) part_nll_s[s] = nll_w;
     if (!more) break;
     cur.assign(nxt);
     il = il1;
@@ -1065,23 +1070,23 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
     f2v accp[RP / 2];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
-    float nll = 0.0f;
+    f2v nll = splat2(0.0f);
     walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
-    nll = wave_sum_dpp(nll) * kLn2;
+    const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (NP == 1) {
 #pragma unroll
       for (int j = 0; j < RP / 2; ++j) {
         if (2 * j < R) slab[((int64_t)t * R + 2 * j) * Kp + k] = accp[j].x;
         if (2 * j + 1 < R) slab[((int64_t)t * R + 2 * j + 1) * Kp + k] = accp[j].y;
       }
-      if (lane == 0) part_nll_c[wi] = nll;
+      if (lane == 0) part_nll_c[wi] = nll_w;
     } else {
 #pragma unroll
       for (int j = 0; j < RP / 2; ++j) {
         if (2 * j < R) Pl[((size_t)u * R + 2 * j) * 64 + lane] = accp[j].x;
         if (2 * j + 1 < R) Pl[((size_t)u * R + 2 * j + 1) * 64 + lane] = accp[j].y;
       }
-      if (lane == 0) Nl[u] = nll;
+      if (lane == 0) Nl[u] = nll_w;
     }
     if (u + NW < U) unit_begin(u + NW);
   }
