@@ -22,6 +22,11 @@ ARCH = os.environ.get("QSC_OFFLOAD_ARCH", "gfx950")
 # lanes into v_pk_* ops costs a v_mov per operand and s_nop hazards in the fused passes.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall",
           "-Wno-unused-function", "-ffp-contract=off", "-fno-slp-vectorize"]
+# per-source flags.  qsc_pass.hip (the fused passes) runs with f32 denormals flushed: the
+# one-bit likelihood carries its tail probability 2^-101 low so that tails below 2^-25 (where the
+# reference's fp32 erf saturates, P == 0) underflow to exactly 0 without a compare per entry
+# (QSC_FTZ_SAT, qsc_common.cuh lik_grad2).
+FILE_FLAGS = {"qsc_pass.hip": ["-fgpu-flush-denormals-to-zero", "-DQSC_FTZ_SAT=1"]}
 
 
 def _hipcc():
@@ -57,7 +62,8 @@ def build(force=False, verbose=True, out=None, extra_flags=()):
         for src in SOURCES:
             obj = os.path.join(tmp, src.replace(".hip", ".o"))
             objs.append(obj)
-            cmd = [hipcc] + CFLAGS + list(extra_flags) + ["-c", os.path.join(CSRC, src), "-o", obj]
+            cmd = ([hipcc] + CFLAGS + FILE_FLAGS.get(src, []) + list(extra_flags) +
+                   ["-c", os.path.join(CSRC, src), "-o", obj])
             procs.append((src, cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE,
                                                      stderr=subprocess.STDOUT)))
         failed = []

@@ -228,6 +228,9 @@ inline Lik make_lik(const qsc_model* m) {
   l.ob_scale = (float)(c / (double)l.a);
   l.ob_thr = (float)((double)l.thr * c / (double)l.a);
   l.ob_kg = (float)((double)p.kgrad / kMillsK);
+#if QSC_FTZ_SAT
+  l.ob_kg = (float)((double)p.kgrad / kMillsK * 0x1p101);  // E is carried 2^-101 low
+#endif
   return l;
 }
 
@@ -339,7 +342,13 @@ __device__ __forceinline__ void lik_grad2(f2v t, int c0, int c1, bool pa, bool p
     if (pa) z.x = kPadZ;
     if (pb) z.y = kPadZ;
     const f2v u = f2v{__builtin_fabsf(z.x), __builtin_fabsf(z.y)};
+#if QSC_FTZ_SAT
+    // T and E carried 2^-101 low: with f32 denormals flushed (the library's qsc_pass build
+    // flag) a tail below 2^-25 underflows to exactly 0 in the products, no compare needed
+    const f2v E = exp2_2(fma2(-z, z, splat2(kMillsLogK - 101.0f)));
+#else
     const f2v E = exp2_2(fma2(-z, z, splat2(kMillsLogK)));  // kMillsK exp(-z^2)
+#endif
     f2v N = u + splat2(kMillsN2);
     N = fma2(N, u, splat2(kMillsN1));
     N = fma2(N, u, splat2(kMillsN0));
@@ -347,8 +356,12 @@ __device__ __forceinline__ void lik_grad2(f2v t, int c0, int c1, bool pa, bool p
     D = fma2(D, u, splat2(kMillsD2));
     D = fma2(D, u, splat2(kMillsD1));
     D = fma2(D, u, splat2(kMillsD0));
+#if QSC_FTZ_SAT
+    const f2v Ts = ((E * N) * rcp2(D)) * splat2(0x1p101f);
+#else
     const f2v T = (E * N) * rcp2(D);
     const f2v Ts = f2v{T.x < kMillsTsat ? 0.0f : T.x, T.y < kMillsTsat ? 0.0f : T.y};
+#endif
     const f2v Q = splat2(1.0f) - Ts;
     const bool z0 = (c0 != 1), z1 = (c1 != 1);
     const bool ta = (z.x < 0.0f) == z0, tb = (z.y < 0.0f) == z1;
@@ -442,6 +455,7 @@ struct AdamScalars {
   float w2;         // fp32(1 - beta2)  (addcmul value)
   float beta2;      // fp32(beta2)      (mul_ scalar)
   float eps;        // fp32(eps)        (add_ scalar)
+  float rbc2;       // hardware rcp(bc2_sqrt): the reciprocal div_fix forms for that divisor
 };
 
 // beta^step for an integer step by binary powering in double (within an ulp of libm pow; the
@@ -467,6 +481,7 @@ __device__ __forceinline__ AdamScalars adam_scalars(const qsc_adam& ad, int step
   s.bc2_sqrt = (float)sqrt(bc2);
   s.w1 = (float)(1.0 - b1);
   s.w2 = (float)(1.0 - b2);
+  s.rbc2 = __builtin_amdgcn_rcpf(s.bc2_sqrt);
   return s;
 }
 
@@ -507,6 +522,51 @@ __device__ __forceinline__ void adam_elem_fast(float& p, float& m, float& v, flo
   v = __builtin_fmaf(__fmul_rn(s.w2, g), g, vb);
   const float denom = __fadd_rn(div_fix(sqrt_fix(v), s.bc2_sqrt), s.eps);
   p = __fadd_rn(p, div_fix(__fmul_rn(-s.step_size, m), denom));
+}
+
+// adam_elem_fast on RH (even) consecutive row elements, two per packed instruction (the S-side
+// Adam of the fused S-pass epilogue and of qsc_supdate), with the S regulariser folded in:
+// g = a + p * coef.  Per element the same operations in the same order as adam_elem_fast (the
+// bc2_sqrt reciprocal is the one div_fix forms), so the results are bitwise those of the scalar
+// form.  Returns sum_j p_new[j]^2 accumulated in j order.
+template <int RH>
+__device__ __forceinline__ float adam_row_fast(float (&p)[RH], float (&m)[RH], float (&v)[RH],
+                                               const float (&a)[RH], float coef,
+                                               const AdamScalars& s) {
+  float nsq = 0.0f;
+#pragma unroll
+  for (int j = 0; j < RH; j += 2) {
+    const f2v pp = f2v{p[j], p[j + 1]}, aa = f2v{a[j], a[j + 1]};
+    const f2v g = aa + pp * splat2(coef);
+    f2v mm = f2v{m[j], m[j + 1]}, vv = f2v{v[j], v[j + 1]};
+    mm = fma2(splat2(s.w1), g - mm, mm);
+    vv = fma2(splat2(s.w2) * g, g, vv * splat2(s.beta2));
+    // sqrt_fix
+    const f2v sq = f2v{__builtin_amdgcn_sqrtf(vv.x), __builtin_amdgcn_sqrtf(vv.y)};
+    const f2v er = fma2(-sq, sq, vv);
+    const f2v hh = splat2(0.5f) * rcp2(sq);
+    const f2v sf = fma2(er, hh, sq);
+    const f2v sx = f2v{vv.x > 0.0f ? sf.x : sq.x, vv.y > 0.0f ? sf.y : sq.y};
+    // div_fix(sx, bc2_sqrt) + eps
+    const f2v q1 = sx * splat2(s.rbc2);
+    const f2v r1 = fma2(-q1, splat2(s.bc2_sqrt), sx);
+    const f2v den = fma2(r1, splat2(s.rbc2), q1) + splat2(s.eps);
+    // div_fix(-step * m, den)
+    const f2v x = splat2(-s.step_size) * mm;
+    const f2v ry = rcp2(den);
+    const f2v q2 = x * ry;
+    const f2v r2 = fma2(-q2, den, x);
+    const f2v pn = pp + fma2(r2, ry, q2);
+    p[j] = pn.x;
+    p[j + 1] = pn.y;
+    m[j] = mm.x;
+    m[j + 1] = mm.y;
+    v[j] = vv.x;
+    v[j + 1] = vv.y;
+  }
+#pragma unroll
+  for (int j = 0; j < RH; ++j) nsq = __builtin_fmaf(p[j], p[j], nsq);
+  return nsq;
 }
 
 }  // namespace qsc

@@ -582,15 +582,13 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
       pv[j] = pick(hmask, sv[j], sv[RH + j]);
     }
     if constexpr (ADAM) {
-      float m[RH], v[RH], nsq = 0.0f;
+      float m[RH], v[RH];
 #pragma unroll
       for (int j = 0; j < RH; ++j) {
         m[j] = cur.mv[j];
         v[j] = cur.vv[j];
-        const float g = __fadd_rn(a[j], __fmul_rn(pv[j], sc.coef));
-        adam_elem_fast(pv[j], m[j], v[j], g, sc.as);
-        nsq = __builtin_fmaf(pv[j], pv[j], nsq);
       }
+      float nsq = adam_row_fast<RH>(pv, m, v, a, sc.coef, sc.as);
       st_row<RH>(S + row + h * RH, pv);
       st_row<RH>(mS + row + h * RH, m);
       st_row<RH>(vS + row + h * RH, v);
@@ -1012,17 +1010,15 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
       acc[2 * j] = half_sum(accp[j].x);
       acc[2 * j + 1] = half_sum(accp[j].y);
     }
-    float a[RH], pv[RH], m[RH], v[RH], nsq = 0.0f;
+    float a[RH], pv[RH], m[RH], v[RH];
 #pragma unroll
     for (int j = 0; j < RH; ++j) {
       a[j] = pick(hmask, acc[j], acc[RH + j]);
       pv[j] = pick(hmask, sv[j], sv[RH + j]);
       m[j] = cur.mv[j];
       v[j] = cur.vv[j];
-      const float g = __fadd_rn(a[j], __fmul_rn(pv[j], sc.coef));
-      adam_elem_fast(pv[j], m[j], v[j], g, sc.as);
-      nsq = __builtin_fmaf(pv[j], pv[j], nsq);
     }
+    float nsq = adam_row_fast<RH>(pv, m, v, a, sc.coef, sc.as);
     const int64_t row = ((int64_t)s * QSC_SLICE + p) * RP;
     st_row<RH>(S + row + h * RH, pv);
     st_row<RH>(mS + row + h * RH, m);
@@ -1363,13 +1359,8 @@ __global__ void __launch_bounds__(kSBlock) supdate_kernel(
   ld_row<RH>(mS + o, m);
   ld_row<RH>(vS + o, v);
   ld_row<RH>(gsrc + o, g);
-  float nsq = 0.0f;
-#pragma unroll
-  for (int j = 0; j < RH; ++j) {
-    const float gg = __fadd_rn(g[j], __fmul_rn(p[j], sc.coef));
-    adam_elem_fast(p[j], m[j], v[j], gg, sc.as);  // the fused S-pass's update (no projection)
-    nsq = __builtin_fmaf(p[j], p[j], nsq);
-  }
+  // the fused S-pass's update (no projection)
+  float nsq = adam_row_fast<RH>(p, m, v, g, sc.coef, sc.as);
   st_row<RH>(S + o, p);
   st_row<RH>(mS + o, m);
   st_row<RH>(vS + o, v);
