@@ -117,9 +117,13 @@ typedef struct qsc_state {
  * that the passes may issue their read-ahead loads without bounds branches. */
 #define QSC_ENTRY_TAIL 256
 /*
- *  C-format ("frequency slices" per pixel tile): tile t (PT positions), k-slice ks (64 k's),
- *     lane l (k = 64*ks + l), entry j < c_width[t*nks+ks]:
+ *  C-format ("frequency slices" per pixel tile): tile t (PT positions), k-slice ks (64 lanes),
+ *     lane l walks bin k = c_kmap[(t*nks+ks)*64 + l], entry j < c_width[t*nks+ks]:
  *     idx = c_off[t*nks+ks] + (j/4)*256 + l*4 + (j%4);  value = qlocal | code << QBITS
+ *     c_kmap: per tile, the bins 0..64*nks-1 (those >= K are empty padding bins) ordered by
+ *     their observation count in the tile, descending (ties: lower k first).  A wave walks its
+ *     64 lists in lockstep, padded to the longest; count-sorted slices keep that padding small
+ *     (C3: 24 % of the entries with k = 64*ks + l, a few % sorted).
  *     Tile rows are whole S-format slices dealt in snake order, so that every tile holds the
  *     same mix of dense and sparse positions (positions are count-sorted): row qlocal of tile t
  *     is position  g*QSC_SLICE + qlocal%QSC_SLICE,  g = i*ntiles + (i odd ? ntiles-1-t : t),
@@ -227,16 +231,18 @@ QSC_API int qsc_obs_count(const uint8_t* codes, int32_t K, int32_t P, int32_t* c
 QSC_API size_t qsc_obs_order_workspace_bytes(int32_t P);
 QSC_API int qsc_obs_order(const int32_t* cnt, int32_t P, int32_t Pp, int32_t* perm, void* ws,
                           size_t ws_bytes, void* stream);
-/* SYNCHRONOUS: computes slice widths/offsets of both formats and fills *desc.
- * s_width[Pp/QSC_SLICE], s_off[Pp/QSC_SLICE + 1], c_width[ntiles*nks], c_off[ntiles*nks + 1]. */
+/* SYNCHRONOUS: computes slice widths/offsets of both formats and the C-format bin order, and
+ * fills *desc.  s_width[Pp/QSC_SLICE], s_off[Pp/QSC_SLICE + 1], c_width[ntiles*nks],
+ * c_off[ntiles*nks + 1], c_kmap[ntiles*nks*64]. */
 QSC_API size_t qsc_obs_layout_workspace_bytes(int32_t K, int32_t P, int32_t PT);
 QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t PT, int32_t nbins,
                            const int32_t* perm, const int32_t* cnt, int32_t* s_width,
-                           int64_t* s_off, int32_t* c_width, int64_t* c_off, void* ws,
-                           size_t ws_bytes, qsc_obs_desc* desc, void* stream);
+                           int64_t* s_off, int32_t* c_width, int64_t* c_off, int32_t* c_kmap,
+                           void* ws, size_t ws_bytes, qsc_obs_desc* desc, void* stream);
 QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* desc, const int32_t* perm,
                          const int32_t* s_width, const int64_t* s_off, const int32_t* c_width,
-                         const int64_t* c_off, void* s_entries, void* c_entries, void* stream);
+                         const int64_t* c_off, const int32_t* c_kmap, void* s_entries,
+                         void* c_entries, void* stream);
 /* gather/scatter between natural pixel order [R][P] and position order [Pp][RP]
  * (RP = qsc_rank_pad(R); rows R..RP-1 and positions of no pixel are zero-filled / ignored) */
 QSC_API int qsc_perm_gather(const float* nat, const int32_t* perm, int32_t R, int32_t P,
@@ -271,8 +277,8 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
                       size_t ws_bytes, void* stream);
 /* C-pass: per-tile partial dC slab + NLL partials into ws. */
 QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_t* c_width,
-                      const int64_t* c_off, const qsc_model* m, int32_t R, const float* S,
-                      const float* C, void* ws, size_t ws_bytes, void* stream);
+                      const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m, int32_t R,
+                      const float* S, const float* C, void* ws, size_t ws_bytes, void* stream);
 /* Fused S-step + next C-pass (free-S solver, Adam on S): one launch equal to qsc_spass(mode 1)
  * followed by qsc_cpass at the updated S -- same partials, same state protocol -- so a solver
  * runs  cpass, cfinish, (scpass, cfinish) x (n-1), spass  for n outer iterations
@@ -281,7 +287,8 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
 QSC_API int qsc_scpass_supported(const qsc_obs_desc* d, int32_t R);
 QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
                        const int64_t* s_off, const void* c_entries, const int32_t* c_width,
-                       const int64_t* c_off, const qsc_model* m, int32_t R, float* S,
+                       const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m, int32_t R,
+                       float* S,
                        const float* C, float* mS, float* vS, const qsc_adam* adam,
                        float lambda_s, qsc_state* st, void* ws, size_t ws_bytes, void* stream);
 /* reduce the C-pass slab (fixed order).  mode 0: write dC (NLL gradient only); mode 1: fused

@@ -53,15 +53,22 @@ __global__ void __launch_bounds__(kBlock) s_width_kernel(const int* __restrict__
   sizes[s] = (int64_t)m * QSC_SLICE;
 }
 
-// C-format per (tile, k) counts via LDS integer atomics (order-independent), then widths.
-__global__ void __launch_bounds__(kBlock) c_width_kernel(const uint8_t* __restrict__ codes,
-                                                         const int* __restrict__ perm, int K,
-                                                         int P, int PT, int nks,
-                                                         int* __restrict__ width,
-                                                         int64_t* __restrict__ sizes) {
-  extern __shared__ int lcnt[];  // [nks*64]
+// C-format layout of one pixel tile (one block per tile): per-bin counts via LDS integer atomics
+// (order-independent), the tile's bins ordered by count, descending, ties by k (padding bins
+// K..Kp-1 count -1, so they come last) -> c_kmap, and per-slice widths (the slice's first, i.e.
+// longest, list rounded up to chunks of 4).  Sorting makes the 64 lists a C-pass wave walks in
+// lockstep near-equal in length (include/qsc.h, C-format).
+__global__ void __launch_bounds__(kBlock) c_layout_kernel(const uint8_t* __restrict__ codes,
+                                                          const int* __restrict__ perm, int K,
+                                                          int P, int PT, int nks,
+                                                          int* __restrict__ width,
+                                                          int64_t* __restrict__ sizes,
+                                                          int* __restrict__ kmap) {
+  extern __shared__ int lcnt[];  // [Kp] counts, then [Kp] bin order
+  const int Kp = nks * 64;
+  int* lord = lcnt + Kp;
   const int t = blockIdx.x;
-  for (int i = threadIdx.x; i < nks * 64; i += blockDim.x) lcnt[i] = 0;
+  for (int i = threadIdx.x; i < Kp; i += blockDim.x) lcnt[i] = i < K ? 0 : -1;
   __syncthreads();
   for (int ql = threadIdx.x; ql < PT; ql += blockDim.x) {
     const int p = perm[tile_pos(t, ql, gridDim.x)];  // grid = one block per tile
@@ -70,9 +77,19 @@ __global__ void __launch_bounds__(kBlock) c_width_kernel(const uint8_t* __restri
       if (codes[(int64_t)k * P + p] != QSC_UNOBSERVED) atomicAdd(&lcnt[k], 1);
   }
   __syncthreads();
+  for (int k = threadIdx.x; k < Kp; k += blockDim.x) {
+    const int c = lcnt[k];
+    int rank = 0;
+    for (int k2 = 0; k2 < Kp; ++k2) {
+      const int c2 = lcnt[k2];
+      rank += (c2 > c) || (c2 == c && k2 < k);
+    }
+    lord[rank] = k;
+    kmap[(int64_t)t * Kp + rank] = k;
+  }
+  __syncthreads();
   for (int ks = threadIdx.x; ks < nks; ks += blockDim.x) {
-    int m = 0;
-    for (int l = 0; l < 64; ++l) m = max(m, lcnt[ks * 64 + l]);
+    int m = max(lcnt[lord[ks * 64]], 0);
     m = (m + 3) & ~3;
     width[(int64_t)t * nks + ks] = m;
     sizes[(int64_t)t * nks + ks] = (int64_t)m * 64;
@@ -135,6 +152,7 @@ __global__ void __launch_bounds__(kBlock) c_fill_kernel(const uint8_t* __restric
                                                         int P, int PT, int nks,
                                                         const int* __restrict__ width,
                                                         const int64_t* __restrict__ off,
+                                                        const int* __restrict__ kmap,
                                                         E* __restrict__ ent) {
   using Tr = EntryTraits<E>;
   const int t = blockIdx.x;
@@ -143,12 +161,13 @@ __global__ void __launch_bounds__(kBlock) c_fill_kernel(const uint8_t* __restric
     const int64_t wi = (int64_t)t * nks + ks;
     const int W = width[wi];
     const int64_t base = off[wi];
+    const int k = kmap[(int64_t)t * nks * 64 + kk];  // the bin of this lane (count-sorted)
     int j = 0;
-    if (kk < K) {
+    if (k < K) {
       for (int ql = 0; ql < PT; ++ql) {
         const int p = perm[tile_pos(t, ql, gridDim.x)];  // grid = one block per tile
         if (p < 0 || p >= P) continue;
-        const uint8_t c = codes[(int64_t)kk * P + p];
+        const uint8_t c = codes[(int64_t)k * P + p];
         if (c != QSC_UNOBSERVED)
           ent[slot(base, 64, lane, j++)] = (E)((uint32_t)ql | ((uint32_t)c << Tr::kBits));
       }
@@ -239,15 +258,15 @@ QSC_API size_t qsc_obs_layout_workspace_bytes(int32_t K, int32_t P, int32_t PT) 
 
 QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t PT, int32_t nbins,
                            const int32_t* perm, const int32_t* cnt, int32_t* s_width,
-                           int64_t* s_off, int32_t* c_width, int64_t* c_off, void* ws,
-                           size_t ws_bytes, qsc_obs_desc* desc, void* stream) {
+                           int64_t* s_off, int32_t* c_width, int64_t* c_off, int32_t* c_kmap,
+                           void* ws, size_t ws_bytes, qsc_obs_desc* desc, void* stream) {
   if (K < 1 || P < 1 || PT < 64 || (PT & 63) || nbins < 1 || nbins > QSC_MAX_BOUNDS - 1 ||
-      !codes || !perm || !cnt || !s_width || !s_off || !c_width || !c_off || !desc || !ws ||
-      ws_bytes < qsc_obs_layout_workspace_bytes(K, P, PT))
+      !codes || !perm || !cnt || !s_width || !s_off || !c_width || !c_off || !c_kmap || !desc ||
+      !ws || ws_bytes < qsc_obs_layout_workspace_bytes(K, P, PT))
     return QSC_EINVAL;
   const int Pp = (int)round_up(P, PT);  // whole tiles; padding positions carry no entries
   const int ns = Pp / QSC_SLICE, nt = Pp / PT, nks = (int)ceil_div(K, 64);
-  if ((int64_t)nks * 64 * sizeof(int) > 64 * 1024) return QSC_EINVAL;  // LDS counters
+  if ((int64_t)nks * 64 * 2 * sizeof(int) > 128 * 1024) return QSC_EINVAL;  // LDS counts + order
   const int wide = (K > 4096 || PT > 4096 || nbins > 15) ? 1 : 0;
   if (wide && ((int64_t)K >= (1 << 24) || (int64_t)PT >= (1 << 24))) return QSC_EINVAL;
   char* w = (char*)ws;
@@ -266,8 +285,8 @@ QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t P
   QSC_TRY(hipMemsetAsync(s_sizes + ns, 0, 8, s));
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(cub, cub_b, s_sizes, s_off, ns + 1, s);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(c_width_kernel, dim3((unsigned)nt), dim3(kBlock), nks * 64 * sizeof(int), s,
-                     codes, perm, K, P, PT, nks, c_width, c_sizes);
+  hipLaunchKernelGGL(c_layout_kernel, dim3((unsigned)nt), dim3(kBlock), nks * 64 * 2 * sizeof(int),
+                     s, codes, perm, K, P, PT, nks, c_width, c_sizes, c_kmap);
   QSC_CHECK_LAUNCH();
   QSC_TRY(hipMemsetAsync(c_sizes + (int64_t)nt * nks, 0, 8, s));
   cub_b = ws_bytes - (size_t)((char*)cub - (char*)ws);
@@ -299,9 +318,10 @@ QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t P
 
 QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* d, const int32_t* perm,
                          const int32_t* s_width, const int64_t* s_off, const int32_t* c_width,
-                         const int64_t* c_off, void* s_entries, void* c_entries, void* stream) {
-  if (!d || !codes || !perm || !s_width || !s_off || !c_width || !c_off || !s_entries ||
-      !c_entries || d->s_entries < QSC_ENTRY_TAIL || d->c_entries < QSC_ENTRY_TAIL)
+                         const int64_t* c_off, const int32_t* c_kmap, void* s_entries,
+                         void* c_entries, void* stream) {
+  if (!d || !codes || !perm || !s_width || !s_off || !c_width || !c_off || !c_kmap ||
+      !s_entries || !c_entries || d->s_entries < QSC_ENTRY_TAIL || d->c_entries < QSC_ENTRY_TAIL)
     return QSC_EINVAL;
   hipStream_t s = STREAM(stream);
   const dim3 tg((QSC_ENTRY_TAIL + kBlock - 1) / kBlock), tb(kBlock);
@@ -315,7 +335,7 @@ QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* d, const int3
                        (uint32_t*)s_entries);
     QSC_CHECK_LAUNCH();
     hipLaunchKernelGGL(c_fill_kernel<uint32_t>, dim3((unsigned)d->ntiles), dim3(kBlock), 0, s,
-                       codes, perm, d->K, d->P, d->PT, d->nks, c_width, c_off,
+                       codes, perm, d->K, d->P, d->PT, d->nks, c_width, c_off, c_kmap,
                        (uint32_t*)c_entries);
   } else {
     hipLaunchKernelGGL(tail_fill_kernel<uint16_t>, tg, tb, 0, s, (uint16_t*)s_entries,
@@ -327,7 +347,7 @@ QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* d, const int3
                        (uint16_t*)s_entries);
     QSC_CHECK_LAUNCH();
     hipLaunchKernelGGL(c_fill_kernel<uint16_t>, dim3((unsigned)d->ntiles), dim3(kBlock), 0, s,
-                       codes, perm, d->K, d->P, d->PT, d->nks, c_width, c_off,
+                       codes, perm, d->K, d->P, d->PT, d->nks, c_width, c_off, c_kmap,
                        (uint16_t*)c_entries);
   }
   QSC_CHECK_LAUNCH();

@@ -625,7 +625,8 @@ constexpr int kCParts = kCBlock / 64;
 template <int RP, typename E, int KIND, bool LOG>
 __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_kernel(
     const E* __restrict__ ent, const int* __restrict__ width, const int64_t* __restrict__ off,
-    int nks, int PT, int xcd_map, Lik lk, Edges E_, int nbins, int R, int K,
+    const int* __restrict__ kmap, int nks, int PT, int xcd_map, Lik lk, Edges E_, int nbins,
+    int R, int K,
     const float* __restrict__ S, const float* __restrict__ C, float* __restrict__ slab,
     float* __restrict__ part_nll, float* __restrict__ cnsq) {
   using T = Ent<E>;
@@ -658,7 +659,7 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   const V4* src = reinterpret_cast<const V4*>(ent + off[wi]) + lane;
   V4 buf[kGroup];
   load_group(src, 64, j0, 1, max(j1 - 1, 0), buf);
-  const int k = ks * 64 + lane;
+  const int k = kmap[wi * 64 + lane];  // this lane's bin (count-sorted order, include/qsc.h)
   float cv[RP];
 #pragma unroll
   for (int r = 0; r < RP; ++r) cv[r] = C[(int64_t)min(r, R - 1) * K + min(k, K - 1)];
@@ -713,7 +714,7 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
 #pragma unroll
     for (int pp = 1; pp < kCParts; ++pp) a += Pl[(size_t)pp * R * 64 + i];
     const int r = i >> 6, l = i & 63;
-    slab[((int64_t)t * R + r) * Kp + ks * 64 + l] = a;
+    slab[((int64_t)t * R + r) * Kp + kmap[wi * 64 + l]] = a;
   }
   if (threadIdx.x == 0) {
     float a = Nl[0];
@@ -744,7 +745,8 @@ constexpr int kCTBlock = 1024;
 template <int RP, typename E, int KIND, bool LOG>
 __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
     const E* __restrict__ ent, const int* __restrict__ width, const int64_t* __restrict__ off,
-    int nks, int NP, int PT, Lik lk, Edges E_, int nbins, int R, int K,
+    const int* __restrict__ kmap, int nks, int NP, int PT, Lik lk, Edges E_, int nbins, int R,
+    int K,
     const float* __restrict__ S, const float* __restrict__ C, float* __restrict__ slab,
     float* __restrict__ part_nll, float* __restrict__ cnsq) {
   using T = Ent<E>;
@@ -769,7 +771,7 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
   int u = w;
   V4 buf[kGroup];
   float cv[RP];
-  int wi = 0, j0 = 0, j1 = 0;
+  int wi = 0, j0 = 0, j1 = 0, k = 0;
   const V4* src = nullptr;
   auto unit_begin = [&](int uu) {
     const int ks = uu / NP, part = uu - ks * NP;
@@ -779,7 +781,7 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
     j1 = (W4 * (part + 1)) / NP;
     src = reinterpret_cast<const V4*>(ent + off[wi]) + lane;
     load_group(src, 64, j0, 1, max(j1 - 1, 0), buf);
-    const int k = ks * 64 + lane;
+    k = kmap[wi * 64 + lane];  // this lane's bin (count-sorted order)
 #pragma unroll
     for (int r = 0; r < RP; ++r) cv[r] = C[(int64_t)min(r, R - 1) * K + min(k, K - 1)];
   };
@@ -802,8 +804,6 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
 
   // 3. units: likelihood + gradient over the part lists
   for (; u < U; u += NW) {
-    const int ks = u / NP;
-    const int k = ks * 64 + lane;
     f2v own[RP / 2];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j)
@@ -845,7 +845,7 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
       float a = p[0];
       for (int pp = 1; pp < NP; ++pp) a += p[(size_t)pp * R * 64];
       const int r = rl >> 6, l = rl & 63;
-      slab[((int64_t)t * R + r) * Kp + ks * 64 + l] = a;
+      slab[((int64_t)t * R + r) * Kp + kmap[((int64_t)t * nks + ks) * 64 + l]] = a;
     }
     for (int ks = threadIdx.x; ks < nks; ks += blockDim.x) {
       float a = Nl[ks * NP];
@@ -887,7 +887,8 @@ template <int RP, typename E, int KIND, bool LOG>
 __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
     const E* __restrict__ s_ent, const int* __restrict__ s_width, const int64_t* __restrict__ s_off,
     const E* __restrict__ c_ent, const int* __restrict__ c_width, const int64_t* __restrict__ c_off,
-    int nks, int NP, int PT, Lik lk, Edges E_, int nbins, int R, int K, float* __restrict__ S,
+    const int* __restrict__ c_kmap, int nks, int NP, int PT, Lik lk, Edges E_, int nbins, int R,
+    int K, float* __restrict__ S,
     const float* __restrict__ C, float* __restrict__ mS, float* __restrict__ vS, qsc_adam ad,
     float lambda_s, qsc_state* __restrict__ st, float* __restrict__ part_nll_s,
     float* __restrict__ part_nsq_s, float* __restrict__ slab, float* __restrict__ part_nll_c,
@@ -1037,7 +1038,7 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
   int u = w;
   V4 buf[kGroup];
   float cv[RP];
-  int wi = 0, j0 = 0, j1 = 0;
+  int wi = 0, j0 = 0, j1 = 0, k = 0;
   const V4* src = nullptr;
   auto unit_begin = [&](int uu) {
     const int ks = uu / NP, part = uu - ks * NP;
@@ -1047,17 +1048,15 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
     j1 = (W4 * (part + 1)) / NP;
     src = reinterpret_cast<const V4*>(c_ent + c_off[wi]) + lane;
     load_group(src, 64, j0, 1, max(j1 - 1, 0), buf);
-    const int k = min(ks * 64 + lane, K - 1);
+    k = c_kmap[wi * 64 + lane];  // this lane's bin (count-sorted order)
 #pragma unroll
-    for (int r = 0; r < RP; ++r) cv[r] = Cl[k * CP + r];  // C_i, as the S-step used
+    for (int r = 0; r < RP; ++r) cv[r] = Cl[min(k, K - 1) * CP + r];  // C_i, as the S-step used
   };
   STAMP(wg, 2);
   if (u < U) unit_begin(u);
   __syncthreads();  // the whole S tile is in LDS
   STAMP(wg, 3);
   for (; u < U; u += NW) {
-    const int ks = u / NP;
-    const int k = ks * 64 + lane;
     f2v own[RP / 2];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j)
@@ -1095,7 +1094,7 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
       float acc = pp0[0];
       for (int pp = 1; pp < NP; ++pp) acc += pp0[(size_t)pp * R * 64];
       const int r = rl >> 6, l = rl & 63;
-      slab[((int64_t)t * R + r) * Kp + ks * 64 + l] = acc;
+      slab[((int64_t)t * R + r) * Kp + c_kmap[((int64_t)t * nks + ks) * 64 + l]] = acc;
     }
     for (int ks = threadIdx.x; ks < nks; ks += blockDim.x) {
       float acc = Nl[ks * NP];
@@ -1585,10 +1584,10 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
 }
 
 QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_t* c_width,
-                      const int64_t* c_off, const qsc_model* m, int32_t R, const float* S,
-                      const float* C, void* ws, size_t ws_bytes, void* stream) {
+                      const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m, int32_t R,
+                      const float* S, const float* C, void* ws, size_t ws_bytes, void* stream) {
   if (!desc_ok(d) || !m || m->nbounds - 1 != d->nbins || R < 1 || R > QSC_MAX_R || !S || !C ||
-      !c_width || !c_off || (d->c_entries > 0 && !c_entries) || !ws ||
+      !c_width || !c_off || !c_kmap || (d->c_entries > 0 && !c_entries) || !ws ||
       ws_bytes < ws_bytes_for(d, R))
     return QSC_EINVAL;
   const int RP = rp_of(R);
@@ -1622,8 +1621,8 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
       const dim3 tb((unsigned)(64 * std::min(U, QSC_CTILE_MAXW)));
 #define CPASS_TILE_LAUNCH(RPV, ET, KD, LG)                                                     \
   hipLaunchKernelGGL((cpass_tile_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles), tb, tshm, \
-                     s, (const ET*)c_entries, c_width, c_off, nks, NP, d->PT, lk, E, d->nbins,   \
-                     R, d->K, S, C, w.slab, w.cnll, w.cnsq)
+                     s, (const ET*)c_entries, c_width, c_off, c_kmap, nks, NP, d->PT, lk, E,     \
+                     d->nbins, R, d->K, S, C, w.slab, w.cnll, w.cnsq)
       QSC_DISPATCH_PASS(CPASS_TILE_LAUNCH);
 #undef CPASS_TILE_LAUNCH
       QSC_CHECK_LAUNCH();
@@ -1634,8 +1633,8 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
   const dim3 grid((unsigned)((int64_t)d->ntiles * d->nks));
 #define CPASS_LAUNCH(RPV, ET, KD, LG)                                                          \
   hipLaunchKernelGGL((cpass_kernel<RPV, ET, KD, LG>), grid, dim3(kCBlock), shm, s,           \
-                     (const ET*)c_entries, c_width, c_off, d->nks, d->PT, xcd_map, lk, E,      \
-                     d->nbins, R, d->K, S, C, w.slab, w.cnll, w.cnsq)
+                     (const ET*)c_entries, c_width, c_off, c_kmap, d->nks, d->PT, xcd_map, lk, \
+                     E, d->nbins, R, d->K, S, C, w.slab, w.cnll, w.cnsq)
   QSC_DISPATCH_PASS(CPASS_LAUNCH);
 #undef CPASS_LAUNCH
   QSC_CHECK_LAUNCH();
@@ -1663,11 +1662,11 @@ QSC_API int qsc_scpass_supported(const qsc_obs_desc* d, int32_t R) {
 
 QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
                        const int64_t* s_off, const void* c_entries, const int32_t* c_width,
-                       const int64_t* c_off, const qsc_model* m, int32_t R, float* S,
-                       const float* C, float* mS, float* vS, const qsc_adam* adam,
+                       const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m, int32_t R,
+                       float* S, const float* C, float* mS, float* vS, const qsc_adam* adam,
                        float lambda_s, qsc_state* st, void* ws, size_t ws_bytes, void* stream) {
   if (!qsc_scpass_supported(d, R) || !m || m->nbounds - 1 != d->nbins || !S || !C || !mS ||
-      !vS || !adam || !st || !s_width || !s_off || !c_width || !c_off ||
+      !vS || !adam || !st || !s_width || !s_off || !c_width || !c_off || !c_kmap ||
       (d->s_entries > 0 && !s_entries) || (d->c_entries > 0 && !c_entries) || !ws ||
       ws_bytes < ws_bytes_for(d, R))
     return QSC_EINVAL;
@@ -1693,7 +1692,7 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
     if constexpr (RPV <= 8)                                                                    \
       hipLaunchKernelGGL((scfused_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles),         \
                          dim3(threads), shm, s, (const ET*)s_entries, s_width, s_off,         \
-                         (const ET*)c_entries, c_width, c_off, d->nks, NP, d->PT, lk, E,       \
+                         (const ET*)c_entries, c_width, c_off, c_kmap, d->nks, NP, d->PT, lk, E, \
                          d->nbins, R, d->K, S, C, mS, vS, ad, lambda_s, st, w.snll, w.snsq,    \
                          w.slab, w.cnll, w.cnsq);                                              \
   } while (0)

@@ -52,8 +52,8 @@ class PassEngine:
     def cpass(self, S_pos, C):
         o = self.obs
         _lib.call("qsc_cpass", o.desc, _lib.ptr(o.c_entries), _lib.ptr(o.c_width), _lib.ptr(o.c_off),
-                  o.model, self.R, _lib.ptr(S_pos), _lib.ptr(C), _lib.ptr(self.ws), self.ws.numel(),
-                  _lib.stream())
+                  _lib.ptr(o.c_kmap), o.model, self.R, _lib.ptr(S_pos), _lib.ptr(C),
+                  _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
 
     def cfinish(self, C, mode, dC=None, mC=None, vC=None, adam=None, lambda_c=0.0,
                 normsq_ext=None, record=True):
@@ -78,7 +78,8 @@ class PassEngine:
         o = self.obs
         _lib.call("qsc_scpass", o.desc, _lib.ptr(o.s_entries), _lib.ptr(o.s_width),
                   _lib.ptr(o.s_off), _lib.ptr(o.c_entries), _lib.ptr(o.c_width),
-                  _lib.ptr(o.c_off), o.model, self.R, _lib.ptr(S_pos), _lib.ptr(C), _lib.ptr(mS),
+                  _lib.ptr(o.c_off), _lib.ptr(o.c_kmap), o.model, self.R, _lib.ptr(S_pos),
+                  _lib.ptr(C), _lib.ptr(mS),
                   _lib.ptr(vS), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),
                   self.ws.numel(), _lib.stream())
 

@@ -100,18 +100,19 @@ class Observations:
         self.s_off = torch.empty(ns + 1, dtype=torch.int64, device=dev)
         self.c_width = torch.empty(nt * nks, dtype=torch.int32, device=dev)
         self.c_off = torch.empty(nt * nks + 1, dtype=torch.int64, device=dev)
+        self.c_kmap = torch.empty(nt * nks * 64, dtype=torch.int32, device=dev)
         desc = _lib.QscObsDesc()
         ws = _ws(_lib.lib().qsc_obs_layout_workspace_bytes(K, P, PT), dev)
         _lib.call("qsc_obs_layout", _lib.ptr(codes), K, P, PT, nbins, _lib.ptr(perm), _lib.ptr(cnt),
                   _lib.ptr(self.s_width), _lib.ptr(self.s_off), _lib.ptr(self.c_width),
-                  _lib.ptr(self.c_off), _lib.ptr(ws), ws.numel(), desc, s)
+                  _lib.ptr(self.c_off), _lib.ptr(self.c_kmap), _lib.ptr(ws), ws.numel(), desc, s)
         self.desc = desc
         et = torch.int32 if desc.wide else torch.int16
         self.s_entries = torch.empty(desc.s_entries, dtype=et, device=dev)
         self.c_entries = torch.empty(desc.c_entries, dtype=et, device=dev)
         _lib.call("qsc_obs_fill", _lib.ptr(codes), desc, _lib.ptr(perm), _lib.ptr(self.s_width),
                   _lib.ptr(self.s_off), _lib.ptr(self.c_width), _lib.ptr(self.c_off),
-                  _lib.ptr(self.s_entries), _lib.ptr(self.c_entries), s)
+                  _lib.ptr(self.c_kmap), _lib.ptr(self.s_entries), _lib.ptr(self.c_entries), s)
 
     # ---- info -----------------------------------------------------------------------
     @property
