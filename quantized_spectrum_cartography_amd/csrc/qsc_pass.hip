@@ -70,12 +70,17 @@ struct Ent<uint16_t> {
   static constexpr int kBits = 12;
   static constexpr uint32_t kMask = 0xFFF;
   static constexpr int kPad = 15;
-  using V4 = uint2;  // 4 entries = 8 bytes
+  using V4 = uint2;     // 4 entries = 8 bytes
+  using V2 = uint32_t;  // 2 entries (half a chunk: the S-pass lane's share)
   __device__ static __forceinline__ void unpack(const V4& v, uint32_t (&e)[4]) {
     e[0] = v.x & 0xFFFF;
     e[1] = v.x >> 16;
     e[2] = v.y & 0xFFFF;
     e[3] = v.y >> 16;
+  }
+  __device__ static __forceinline__ void unpack2(const V2& v, uint32_t (&e)[2]) {
+    e[0] = v & 0xFFFF;
+    e[1] = v >> 16;
   }
 };
 template <>
@@ -84,11 +89,16 @@ struct Ent<uint32_t> {
   static constexpr uint32_t kMask = 0xFFFFFF;
   static constexpr int kPad = 255;
   using V4 = uint4;  // 4 entries = 16 bytes
+  using V2 = uint2;  // 2 entries
   __device__ static __forceinline__ void unpack(const V4& v, uint32_t (&e)[4]) {
     e[0] = v.x;
     e[1] = v.y;
     e[2] = v.z;
     e[3] = v.w;
+  }
+  __device__ static __forceinline__ void unpack2(const V2& v, uint32_t (&e)[2]) {
+    e[0] = v.x;
+    e[1] = v.y;
   }
 };
 
@@ -144,27 +154,24 @@ struct Scalars {
 // moves them to z' = kPadZ where they contribute exactly 0, the other kinds mask them.  The NLL
 // is accumulated as a pair (summed by the caller).
 template <int RP, typename E, int KIND, bool LOG>
-__device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const f2v (&own)[RP / 2],
-                                      const float* __restrict__ tab,
-                                      const float2* __restrict__ edges, const Lik& lk,
-                                      f2v (&acc)[RP / 2], f2v& nll, bool valid = true) {
+__device__ __forceinline__ void pair_step(uint32_t ea, uint32_t eb, const f2v (&own)[RP / 2],
+                                          const float* __restrict__ tab,
+                                          const float2* __restrict__ edges, const Lik& lk,
+                                          f2v (&acc)[RP / 2], f2v& nll, bool valid) {
   using T = Ent<E>;
-  uint32_t e[4];
-  T::unpack(v, e);
-#pragma unroll
-  for (int u = 0; u < 4; u += 2) {
-    const int ca = (int)(e[u] >> T::kBits), cb = (int)(e[u + 1] >> T::kBits);
+  {
+    const int ca = (int)(ea >> T::kBits), cb = (int)(eb >> T::kBits);
     const bool pa = (ca == T::kPad) || !valid, pb = (cb == T::kPad) || !valid;
     f2v oa[RP / 2], ob[RP / 2];
 #if QSC_DIAG_NOLDS  // diagnostic build: no gather (bounds the LDS share of the pass)
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) {
-      oa[j] = own[j] + splat2((float)(e[u] & T::kMask));
-      ob[j] = own[j] + splat2((float)(e[u + 1] & T::kMask));
+      oa[j] = own[j] + splat2((float)(ea & T::kMask));
+      ob[j] = own[j] + splat2((float)(eb & T::kMask));
     }
 #else
-    lds_row2<RP>(tab + (e[u] & T::kMask) * Pitch<RP>::v, oa);
-    lds_row2<RP>(tab + (e[u + 1] & T::kMask) * Pitch<RP>::v, ob);
+    lds_row2<RP>(tab + (ea & T::kMask) * Pitch<RP>::v, oa);
+    lds_row2<RP>(tab + (eb & T::kMask) * Pitch<RP>::v, ob);
 #endif
     f2v t;
     if constexpr (KIND == LIK_ONEBIT)
@@ -194,6 +201,29 @@ __device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const f2v (&
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) acc[j] = fma2(splat2(gb), ob[j], acc[j]);
   }
+}
+
+// one 4-entry chunk (the C-pass lane's unit) as two pairs
+template <int RP, typename E, int KIND, bool LOG>
+__device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const f2v (&own)[RP / 2],
+                                      const float* __restrict__ tab,
+                                      const float2* __restrict__ edges, const Lik& lk,
+                                      f2v (&acc)[RP / 2], f2v& nll, bool valid = true) {
+  uint32_t e[4];
+  Ent<E>::unpack(v, e);
+  pair_step<RP, E, KIND, LOG>(e[0], e[1], own, tab, edges, lk, acc, nll, valid);
+  pair_step<RP, E, KIND, LOG>(e[2], e[3], own, tab, edges, lk, acc, nll, valid);
+}
+
+// half a chunk (the S-pass lane's unit: the pixel's two lanes split every chunk)
+template <int RP, typename E, int KIND, bool LOG>
+__device__ __forceinline__ void half_chunk(const typename Ent<E>::V2& v, const f2v (&own)[RP / 2],
+                                           const float* __restrict__ tab,
+                                           const float2* __restrict__ edges, const Lik& lk,
+                                           f2v (&acc)[RP / 2], f2v& nll) {
+  uint32_t e[2];
+  Ent<E>::unpack2(v, e);
+  pair_step<RP, E, KIND, LOG>(e[0], e[1], own, tab, edges, lk, acc, nll, true);
 }
 
 // Read-ahead of a lane list in groups of NB chunks (chunk j at src[j * row], row in V4 units).
@@ -237,6 +267,40 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
     if (!more) break;
 #pragma unroll
     for (int i = 0; i < kGroup; ++i) b[i] = nb[i];
+    jb = jn;
+  }
+}
+
+// S-pass form: the pixel's two lanes split every 4-entry chunk (lane half h takes entries 2h,
+// 2h+1 of each chunk row), so both walk the same, wave-uniform chunk range [0, j1) with one
+// entry pair per chunk row -- no lane idles on an odd chunk count (C3: 12 % -> 6 % padded
+// evaluations).  Group b holds chunk rows jb .. jb+kGroupS-1 (src[j * row]); the next group is
+// read ahead unconditionally (clamped to the last row: static vmcnt accounting).
+constexpr int kGroupS = 8;
+
+template <int RP, typename E, int KIND, bool LOG>
+__device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restrict__ src, int row,
+                                            int j1, typename Ent<E>::V2 (&b)[kGroupS],
+                                            const f2v (&own)[RP / 2],
+                                            const float* __restrict__ tab,
+                                            const float2* __restrict__ edges, const Lik& lk,
+                                            f2v (&acc)[RP / 2], f2v& nll) {
+  using V2 = typename Ent<E>::V2;
+  j1 = __builtin_amdgcn_readfirstlane(j1);
+  const int jlast = max(j1 - 1, 0);
+  int jb = 0;
+  for (;;) {
+    const int jn = jb + kGroupS;
+    const bool more = jn < j1;
+    V2 nb[kGroupS];
+#pragma unroll
+    for (int i = 0; i < kGroupS; ++i) nb[i] = src[(int64_t)min(jn + i, jlast) * row];
+#pragma unroll
+    for (int i = 0; i < kGroupS; ++i)
+      if (jb + i < j1) half_chunk<RP, E, KIND, LOG>(b[i], own, tab, edges, lk, acc, nll);
+    if (!more) break;
+#pragma unroll
+    for (int i = 0; i < kGroupS; ++i) b[i] = nb[i];
     jb = jn;
   }
 }
@@ -397,15 +461,15 @@ __device__ __forceinline__ void st_row(float* __restrict__ dst, const float (&v)
 // the moments of the lane's rows.  Two sets live at once (current + prefetched next slice).
 template <int RP, typename E, bool ADAM>
 struct SliceIn {
-  typename Ent<E>::V4 buf[kGroup];
+  typename Ent<E>::V2 buf[kGroupS];
   float sv[RP];
   float mv[RP / 2], vv[RP / 2];
   int j1;
-  const typename Ent<E>::V4* src;
+  const typename Ent<E>::V2* src;
 
   __device__ __forceinline__ void assign(const SliceIn& o) {
 #pragma unroll
-    for (int i = 0; i < kGroup; ++i) buf[i] = o.buf[i];
+    for (int i = 0; i < kGroupS; ++i) buf[i] = o.buf[i];
 #pragma unroll
     for (int r = 0; r < RP; ++r) sv[r] = o.sv[r];
     if constexpr (ADAM) {
@@ -421,6 +485,8 @@ struct SliceIn {
 };
 
 // Issue every global read of slice s for this lane (unconditional loads: static vmcnt).
+// Entries: the lane's half (entries 2h, 2h+1) of its position's chunk in each chunk row of
+// QSC_SLICE positions (2 * QSC_SLICE halves per row), the first kGroupS rows.
 // Position-order rows are [Pp][RP]: the lane reads its pixel's whole S row and the half
 // [h*RP/2, (h+1)*RP/2) of the Adam moments it will update.
 template <int RP, typename E, bool ADAM>
@@ -430,10 +496,12 @@ __device__ __forceinline__ void slice_load(SliceIn<RP, E, ADAM>& in, const E* __
                                            const float* __restrict__ S,
                                            const float* __restrict__ mS,
                                            const float* __restrict__ vS) {
-  using V4 = typename Ent<E>::V4;
+  using V2 = typename Ent<E>::V2;
   in.j1 = width[s] >> 2;
-  in.src = reinterpret_cast<const V4*>(ent + off[s]) + p;
-  load_group(in.src, QSC_SLICE, h, 2, max(in.j1 - 1, 0), in.buf);
+  in.src = reinterpret_cast<const V2*>(ent + off[s]) + 2 * p + h;
+  const int jlast = max(in.j1 - 1, 0);
+#pragma unroll
+  for (int i = 0; i < kGroupS; ++i) in.buf[i] = in.src[(int64_t)min(i, jlast) * (2 * QSC_SLICE)];
   const int64_t row = ((int64_t)s * QSC_SLICE + p) * RP;
   ld_row<RP>(S + row, in.sv);
   if constexpr (ADAM) {
@@ -557,13 +625,8 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-#if QSC_SPASS_MASKED
-    walk_masked<RP, E, KIND, LOG>(cur.src, QSC_SLICE, h, 0, cur.j1, 2, cur.buf, own, Cl, El, lk,
-                                  accp, nll);
-#else
-    walk_groups<RP, E, KIND, LOG>(cur.src, QSC_SLICE, h, cur.j1, 2, cur.buf, own, Cl, El, lk,
-                                  accp, nll);
-#endif
+    walk_halves<RP, E, KIND, LOG>(cur.src, 2 * QSC_SLICE, cur.j1, cur.buf, own, Cl, El, lk, accp,
+                                  nll);
     STAMP(w, 3 + 3 * i);
     // the two lane halves' partial dS: v_permlane32_swap (VALU) instead of an LDS shuffle
     float acc[RP];
@@ -1003,8 +1066,8 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_groups<RP, E, KIND, LOG>(cur.src, QSC_SLICE, h, cur.j1, 2, cur.buf, own, Cl, El, lk,
-                                  accp, nll);
+    walk_halves<RP, E, KIND, LOG>(cur.src, 2 * QSC_SLICE, cur.j1, cur.buf, own, Cl, El, lk, accp,
+                                  nll);
     float acc[RP];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) {
