@@ -39,6 +39,10 @@ constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 #ifndef QSC_SPASS_WAVES
 #define QSC_SPASS_WAVES 4
 #endif
+// fused launch: waves that read their first slice before the staging barrier (see scfused)
+#ifndef QSC_EARLY_WAVES
+#define QSC_EARLY_WAVES 16
+#endif
 #ifndef QSC_CPASS_WAVES
 #define QSC_CPASS_WAVES 4
 #endif
@@ -101,6 +105,18 @@ struct Ent<uint32_t> {
     e[1] = v.y;
   }
 };
+
+// Per-lane global access at byte offset `lo` (32 bits) from a wave-uniform base: the address is
+// SGPR base + zero-extended VGPR offset (the global_load/store saddr form), so the per-access
+// 64-bit address arithmetic stays on the scalar unit instead of costing VALU per load.
+template <typename T>
+__device__ __forceinline__ T ld_lane(const T* base, uint32_t lo) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + lo);
+}
+template <typename T>
+__device__ __forceinline__ void st_lane(T* base, uint32_t lo, const T& v) {
+  *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + lo) = v;
+}
 
 // LDS row of RP floats as RP/2 packed pairs (16-B reads)
 template <int RP>
@@ -235,20 +251,20 @@ constexpr int kGroup = 4;
 constexpr int kSchedQ = 16;  // S-pass slice queues (scheduler counters), QSC_PASS workspace
 
 template <typename V4>
-__device__ __forceinline__ void load_group(const V4* __restrict__ src, int row, int jb, int js,
-                                           int jlast, V4 (&b)[kGroup]) {
+__device__ __forceinline__ void load_group(const V4* __restrict__ src, uint32_t lo, int row, int jb,
+                                           int js, int jlast, V4 (&b)[kGroup]) {
 #pragma unroll
   for (int i = 0; i < kGroup; ++i) {
     const int j = min(jb + i * js, jlast);
-    b[i] = src[(int64_t)j * row];
+    b[i] = ld_lane(src + (int64_t)j * row, lo);
   }
 }
 
 // Consume group b (chunks jb, jb+js, ..., < j1), then walk the rest of the list with the next
 // group's loads issued ahead of the current group's arithmetic.
 template <int RP, typename E, int KIND, bool LOG>
-__device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restrict__ src, int row,
-                                            int jb, int j1, int js,
+__device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restrict__ src,
+                                            uint32_t lo, int row, int jb, int j1, int js,
                                             typename Ent<E>::V4 (&b)[kGroup],
                                             const f2v (&own)[RP / 2],
                                             const float* __restrict__ tab,
@@ -260,7 +276,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
     const int jn = jb + kGroup * js;
     const bool more = jn < j1;
     V4 nb[kGroup];
-    load_group(src, row, jn, js, jlast, nb);  // unconditional: static vmcnt accounting
+    load_group(src, lo, row, jn, js, jlast, nb);  // unconditional: static vmcnt accounting
 #pragma unroll
     for (int i = 0; i < kGroup; ++i)
       if (jb + i * js < j1) chunk<RP, E, KIND, LOG>(b[i], own, tab, edges, lk, acc, nll);
@@ -279,8 +295,9 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
 constexpr int kGroupS = 8;
 
 template <int RP, typename E, int KIND, bool LOG>
-__device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restrict__ src, int row,
-                                            int j1, typename Ent<E>::V2 (&b)[kGroupS],
+__device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restrict__ src,
+                                            uint32_t lo, int row, int j1,
+                                            typename Ent<E>::V2 (&b)[kGroupS],
                                             const f2v (&own)[RP / 2],
                                             const float* __restrict__ tab,
                                             const float2* __restrict__ edges, const Lik& lk,
@@ -294,7 +311,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
     const bool more = jn < j1;
     V2 nb[kGroupS];
 #pragma unroll
-    for (int i = 0; i < kGroupS; ++i) nb[i] = src[(int64_t)min(jn + i, jlast) * row];
+    for (int i = 0; i < kGroupS; ++i) nb[i] = ld_lane(src + (int64_t)min(jn + i, jlast) * row, lo);
 #pragma unroll
     for (int i = 0; i < kGroupS; ++i)
       if (jb + i < j1) half_chunk<RP, E, KIND, LOG>(b[i], own, tab, edges, lk, acc, nll);
@@ -312,8 +329,8 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
 // chunk of the wave's lanes, `j1` the (uniform) list end.  The next group is read only when
 // some lane needs it.
 template <int RP, typename E, int KIND, bool LOG>
-__device__ __forceinline__ void walk_masked(const typename Ent<E>::V4* __restrict__ src, int row,
-                                            int jb, int ju, int j1, int js,
+__device__ __forceinline__ void walk_masked(const typename Ent<E>::V4* __restrict__ src,
+                                            uint32_t lo, int row, int jb, int ju, int j1, int js,
                                             typename Ent<E>::V4 (&b)[kGroup],
                                             const f2v (&own)[RP / 2],
                                             const float* __restrict__ tab,
@@ -335,7 +352,7 @@ __device__ __forceinline__ void walk_masked(const typename Ent<E>::V4* __restric
       break;
     }
     V4 nb[kGroup];
-    load_group(src, row, jn, js, jlast, nb);
+    load_group(src, lo, row, jn, js, jlast, nb);
 #pragma unroll
     for (int i = 0; i < kGroup; ++i)
       chunk<RP, E, KIND, LOG>(b[i], own, tab, edges, lk, acc, nll, jb + i * js < j1);
@@ -457,6 +474,36 @@ __device__ __forceinline__ void st_row(float* __restrict__ dst, const float (&v)
   }
 }
 
+// The same at byte offset `lo` from a wave-uniform base (ld_lane / st_lane: saddr form)
+template <int N>
+__device__ __forceinline__ void ld_row(const float* __restrict__ base, uint32_t lo, float (&v)[N]) {
+  if constexpr (N == 2) {
+    const float2 x = ld_lane(reinterpret_cast<const float2*>(base), lo);
+    v[0] = x.x;
+    v[1] = x.y;
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; i += 4) {
+      const float4 x = ld_lane(reinterpret_cast<const float4*>(base), lo + 4 * i);
+      v[i] = x.x;
+      v[i + 1] = x.y;
+      v[i + 2] = x.z;
+      v[i + 3] = x.w;
+    }
+  }
+}
+template <int N>
+__device__ __forceinline__ void st_row(float* __restrict__ base, uint32_t lo, const float (&v)[N]) {
+  if constexpr (N == 2) {
+    st_lane(reinterpret_cast<float2*>(base), lo, make_float2(v[0], v[1]));
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; i += 4)
+      st_lane(reinterpret_cast<float4*>(base), lo + 4 * i,
+              make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]));
+  }
+}
+
 // Per-slice registers read from HBM: the first group of entry chunks, S[:, q] and (fused Adam)
 // the moments of the lane's rows.  Two sets live at once (current + prefetched next slice).
 template <int RP, typename E, bool ADAM>
@@ -465,7 +512,7 @@ struct SliceIn {
   float sv[RP];
   float mv[RP / 2], vv[RP / 2];
   int j1;
-  const typename Ent<E>::V2* src;
+  const typename Ent<E>::V2* src;  // the slice's entries (wave-uniform; lanes add SliceLane::ent)
 
   __device__ __forceinline__ void assign(const SliceIn& o) {
 #pragma unroll
@@ -489,24 +536,39 @@ struct SliceIn {
 // QSC_SLICE positions (2 * QSC_SLICE halves per row), the first kGroupS rows.
 // Position-order rows are [Pp][RP]: the lane reads its pixel's whole S row and the half
 // [h*RP/2, (h+1)*RP/2) of the Adam moments it will update.
+// Per-lane byte offsets of the S-pass accesses (constant for a lane): its entry half within a
+// chunk row, its pixel's S row and its half of that row within a slice's block of rows.
+struct SliceLane {
+  uint32_t ent, row, half;
+};
+template <int RP, typename E>
+__device__ __forceinline__ SliceLane slice_lane(int p, int h) {
+  SliceLane l;
+  l.ent = (uint32_t)(2 * p + h) * (uint32_t)sizeof(typename Ent<E>::V2);
+  l.row = (uint32_t)(p * RP) * 4u;
+  l.half = l.row + (uint32_t)(h * (RP / 2)) * 4u;
+  return l;
+}
+
 template <int RP, typename E, bool ADAM>
 __device__ __forceinline__ void slice_load(SliceIn<RP, E, ADAM>& in, const E* __restrict__ ent,
                                            const int* __restrict__ width,
-                                           const int64_t* __restrict__ off, int s, int p, int h,
-                                           const float* __restrict__ S,
+                                           const int64_t* __restrict__ off, int s,
+                                           const SliceLane& ln, const float* __restrict__ S,
                                            const float* __restrict__ mS,
                                            const float* __restrict__ vS) {
   using V2 = typename Ent<E>::V2;
   in.j1 = width[s] >> 2;
-  in.src = reinterpret_cast<const V2*>(ent + off[s]) + 2 * p + h;
+  in.src = reinterpret_cast<const V2*>(ent + off[s]);
   const int jlast = max(in.j1 - 1, 0);
 #pragma unroll
-  for (int i = 0; i < kGroupS; ++i) in.buf[i] = in.src[(int64_t)min(i, jlast) * (2 * QSC_SLICE)];
-  const int64_t row = ((int64_t)s * QSC_SLICE + p) * RP;
-  ld_row<RP>(S + row, in.sv);
+  for (int i = 0; i < kGroupS; ++i)
+    in.buf[i] = ld_lane(in.src + (int64_t)min(i, jlast) * (2 * QSC_SLICE), ln.ent);
+  const int64_t blk = (int64_t)s * QSC_SLICE * RP;  // the slice's rows (uniform)
+  ld_row<RP>(S + blk, ln.row, in.sv);
   if constexpr (ADAM) {
-    ld_row<RP / 2>(mS + row + h * (RP / 2), in.mv);
-    ld_row<RP / 2>(vS + row + h * (RP / 2), in.vv);
+    ld_row<RP / 2>(mS + blk, ln.half, in.mv);
+    ld_row<RP / 2>(vS + blk, ln.half, in.vv);
   }
 }
 
@@ -519,7 +581,8 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     int nslices, Lik lk, Edges E_, int nbins, int R, int K, int Pp, float* __restrict__ S,
     const float* __restrict__ C, float* __restrict__ dS, float* __restrict__ mS,
     float* __restrict__ vS, qsc_adam ad, float lambda_s, qsc_state* __restrict__ st,
-    float* __restrict__ part_nll, float* __restrict__ part_nsq, int* __restrict__ sched) {
+    float* __restrict__ part_nll, float* __restrict__ part_nsq, int* __restrict__ sched,
+    AdamCache* __restrict__ acache) {
   constexpr int CP = Pitch<RP>::v;
   constexpr int RH = RP / 2;  // row elements updated per lane (half row)
   // linear models evaluate the entries in a scaled form (lik_grad2)
@@ -531,8 +594,8 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
   float2* El = reinterpret_cast<float2*>(Cl + (size_t)K * CP);  // [nbins]
 
   // a wave = one slice of QSC_SLICE (32) pixel positions at a time, two lanes per pixel: lane
-  // half h walks the pixel's chunks h, h+2, ...; the halves' partial dS are summed by a lane
-  // swap and each half then updates its half of the pixel's row
+  // half h takes entries 2h, 2h+1 of every 4-entry chunk of the pixel's list; the halves'
+  // partial dS are summed by a lane swap and each half then updates its half of the pixel's row
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int p = lane & (QSC_SLICE - 1), h = lane >> 5;
@@ -560,9 +623,10 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
   const float2 e0 = E_.e[min(k0, nbins - 1)];
   __builtin_amdgcn_sched_barrier(0);
   SliceIn<RP, E, ADAM> cur;
+  const SliceLane ln = slice_lane<RP, E>(p, h);
   // unconditional (a wave without slices reads slice 0): a static load count lets the C^T
   // staging below wait for its own reads only
-  slice_load(cur, ent, width, off, s < nslices ? s : 0, p, h, S, mS, vS);
+  slice_load(cur, ent, width, off, s < nslices ? s : 0, ln, S, mS, vS);
   // 2. stage C^T (rows padded to CP) and the bin edges in LDS
   {
     // branch-free (threads past K rewrite row K-1 with its own values), so the C^T reads stay
@@ -588,7 +652,8 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     if (ADAM) {
       const float nrm = sqrtf(st->normsq_s);
       sc.coef = nrm > 0.0f ? lambda_s / nrm : 0.0f;
-      sc.as = adam_scalars(ad, st->step_s + 1);
+      const int step = st->step_s + 1;
+      sc.as = adam_scalars_cached(acache[step & 1], ad, step);
     }
     if (blockIdx.x == 0) {
       // book-keeping (fields no block of this kernel reads): see qsc_state
@@ -603,19 +668,20 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
   __syncthreads();
   STAMP(w, 1);
 
+  // one slice: the next slice's reads (into q) in flight during this slice's (c) arithmetic;
+  // the loop below alternates the two register sets instead of copying q into c
   int i = 0;
-  while (s < nslices) {
+  auto one_slice = [&](SliceIn<RP, E, ADAM>& c, SliceIn<RP, E, ADAM>& q) -> bool {
     const int s1 = slice_of(i + 1);
     const bool more = s1 < nslices;  // wave-uniform
-    // 3. next slice's reads in flight during this slice's arithmetic (unconditional: a last
-    //    slice re-reads itself, cache-resident, so the wait counts stay static)
-    SliceIn<RP, E, ADAM> nxt;
-    slice_load(nxt, ent, width, off, more ? s1 : s, p, h, S, mS, vS);
+    // 3. next slice's reads (unconditional: a last slice re-reads itself, cache-resident, so
+    //    the wait counts stay static)
+    slice_load(q, ent, width, off, more ? s1 : s, ln, S, mS, vS);
     STAMP(w, 2 + 3 * i);
-    const int64_t row = ((int64_t)s * QSC_SLICE + p) * RP;
+    const int64_t blk = (int64_t)s * QSC_SLICE * RP;  // the slice's rows (uniform)
     float sv[RP];  // rows >= R are zero in HBM (position-order padding)
 #pragma unroll
-    for (int r = 0; r < RP; ++r) sv[r] = cur.sv[r];
+    for (int r = 0; r < RP; ++r) sv[r] = c.sv[r];
     f2v own[RP / 2];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) own[j] = f2v{sv[2 * j], sv[2 * j + 1]} * splat2(own_scale);
@@ -625,8 +691,8 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_halves<RP, E, KIND, LOG>(cur.src, 2 * QSC_SLICE, cur.j1, cur.buf, own, Cl, El, lk, accp,
-                                  nll);
+    walk_halves<RP, E, KIND, LOG>(c.src, ln.ent, 2 * QSC_SLICE, c.j1, c.buf, own, Cl, El, lk,
+                                  accp, nll);
     STAMP(w, 3 + 3 * i);
     // the two lane halves' partial dS: v_permlane32_swap (VALU) instead of an LDS shuffle
     float acc[RP];
@@ -648,26 +714,34 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
       float m[RH], v[RH];
 #pragma unroll
       for (int j = 0; j < RH; ++j) {
-        m[j] = cur.mv[j];
-        v[j] = cur.vv[j];
+        m[j] = c.mv[j];
+        v[j] = c.vv[j];
       }
       float nsq = adam_row_fast<RH>(pv, m, v, a, sc.coef, sc.as);
-      st_row<RH>(S + row + h * RH, pv);
-      st_row<RH>(mS + row + h * RH, m);
-      st_row<RH>(vS + row + h * RH, v);
+      st_row<RH>(S + blk, ln.half, pv);
+      st_row<RH>(mS + blk, ln.half, m);
+      st_row<RH>(vS + blk, ln.half, v);
       nsq = wave_sum_dpp(nsq);
       if (lane == 0) part_nsq[s] = nsq;
     } else {
-      st_row<RH>(dS + row + h * RH, a);
+      st_row<RH>(dS + blk, ln.half, a);
     }
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (lane == 0) part_nll[s] = nll_w;
     STAMP(w, 4 + 3 * i);
-    if (!more) break;
-    cur.assign(nxt);
     s = s1;
     ++i;
+    return more;
+  };
+  if (s < nslices) {
+    SliceIn<RP, E, ADAM> nxt;
+    for (;;) {
+      if (!one_slice(cur, nxt)) break;
+      if (!one_slice(nxt, cur)) break;
+    }
   }
+  // the next S-step's scalars (cfinish settles step_s + 1 in between)
+  if (ADAM && blockIdx.x == 0 && threadIdx.x == 0) adam_cache_store(acache, ad, st->step_s + 2);
   STAMP(w, kStampLast);
   RSTAMP(w, 29);
 }
@@ -719,9 +793,10 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   const int64_t wi = (int64_t)t * nks + ks;
   const int W4 = width[wi] >> 2;
   const int j0 = (W4 * part) / kCParts, j1 = (W4 * (part + 1)) / kCParts;
-  const V4* src = reinterpret_cast<const V4*>(ent + off[wi]) + lane;
+  const V4* src = reinterpret_cast<const V4*>(ent + off[wi]);
+  const uint32_t lo = (uint32_t)lane * (uint32_t)sizeof(V4);
   V4 buf[kGroup];
-  load_group(src, 64, j0, 1, max(j1 - 1, 0), buf);
+  load_group(src, lo, 64, j0, 1, max(j1 - 1, 0), buf);
   const int k = kmap[wi * 64 + lane];  // this lane's bin (count-sorted order, include/qsc.h)
   float cv[RP];
 #pragma unroll
@@ -756,9 +831,9 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
   f2v nll = splat2(0.0f);
 #if QSC_CPASS_MASKED
-  walk_masked<RP, E, KIND, LOG>(src, 64, j0, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+  walk_masked<RP, E, KIND, LOG>(src, lo, 64, j0, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
 #else
-  walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+  walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
 #endif
   STAMP(wg, 2);
   const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
@@ -836,14 +911,15 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
   float cv[RP];
   int wi = 0, j0 = 0, j1 = 0, k = 0;
   const V4* src = nullptr;
+  const uint32_t lo = (uint32_t)lane * (uint32_t)sizeof(V4);
   auto unit_begin = [&](int uu) {
     const int ks = uu / NP, part = uu - ks * NP;
     wi = t * nks + ks;
     const int W4 = width[wi] >> 2;
     j0 = (W4 * part) / NP;
     j1 = (W4 * (part + 1)) / NP;
-    src = reinterpret_cast<const V4*>(ent + off[wi]) + lane;
-    load_group(src, 64, j0, 1, max(j1 - 1, 0), buf);
+    src = reinterpret_cast<const V4*>(ent + off[wi]);
+    load_group(src, lo, 64, j0, 1, max(j1 - 1, 0), buf);
     k = kmap[wi * 64 + lane];  // this lane's bin (count-sorted order)
 #pragma unroll
     for (int r = 0; r < RP; ++r) cv[r] = C[(int64_t)min(r, R - 1) * K + min(k, K - 1)];
@@ -876,7 +952,7 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (NP == 1) {
       // the unit is the whole (tile, k-slice): its slab rows straight from registers
@@ -955,7 +1031,7 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
     const float* __restrict__ C, float* __restrict__ mS, float* __restrict__ vS, qsc_adam ad,
     float lambda_s, qsc_state* __restrict__ st, float* __restrict__ part_nll_s,
     float* __restrict__ part_nsq_s, float* __restrict__ slab, float* __restrict__ part_nll_c,
-    float* __restrict__ cnsq) {
+    float* __restrict__ cnsq, AdamCache* __restrict__ acache) {
   using V4 = typename Ent<E>::V4;
   constexpr int CP = Pitch<RP>::v;  // C^T row pitch == S tile row pitch
   constexpr int RH = RP / 2;
@@ -982,6 +1058,9 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
   [[maybe_unused]] const int wg = blockIdx.x * (kCTBlock / 64) + w;  // (diagnostic stamps)
   STAMP(wg, 0);
   RSTAMP(wg, 28);
+#if QSC_DIAG_STAMPS
+  if (lane == 0 && wg < kStampWaves) g_stamps[wg * kStamps + 26] = __builtin_amdgcn_s_getreg(0xF804);
+#endif
 
   // 1. C^T / edge / state reads first (the LDS staging then waits only for them: vmcnt
   //    retires in issue order), then the first slice's reads, then the staging
@@ -992,47 +1071,64 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
   const float2 e0 = E_.e[min(k0, nbins - 1)];
   float nsq_s = 0.0f;
   int step_s = 0;
+  AdamCache ac0{}, ac1{};
   if (threadIdx.x == 0) {
     nsq_s = st->normsq_s;
     step_s = st->step_s;
+    ac0 = acache[0];  // both slots: no dependent read on step_s
+    ac1 = acache[1];
   }
   __builtin_amdgcn_sched_barrier(0);
   int il = local_of(0);
   SliceIn<RP, E, ADAM> cur;
-  slice_load(cur, s_ent, s_width, s_off, global_of(il < nsl ? il : 0), p, h, S, mS, vS);
-  {
+  const SliceLane ln = slice_lane<RP, E>(p, h);
+  // Staggered first reads: a SIMD runs its waves nearly one after another (oldest first), so
+  // only the oldest wave of each SIMD (w < QSC_EARLY_WAVES) reads its first slice now; the
+  // others read theirs after the staging barrier, while the oldest ones compute.  The first
+  // burst is then a quarter of the tile's slice data and the S-step starts that much earlier.
+  const bool early = w < QSC_EARLY_WAVES;
+  auto stage = [&]() {
     const int kw = min(k0, K - 1);  // branch-free: threads past K rewrite row K-1
 #pragma unroll
     for (int r = 0; r < RP; r += 4)
       *reinterpret_cast<float4*>(Cl + kw * CP + r) =
           make_float4(r < R ? c0[r] : 0.0f, r + 1 < R ? c0[r + 1] : 0.0f,
                       r + 2 < R ? c0[r + 2] : 0.0f, r + 3 < R ? c0[r + 3] : 0.0f);
-  }
-  for (int k = k0 + (int)blockDim.x; k < K; k += blockDim.x) {
-    float v[RP];
+    for (int k = k0 + (int)blockDim.x; k < K; k += blockDim.x) {
+      float v[RP];
 #pragma unroll
-    for (int r = 0; r < RP; ++r) v[r] = (r < R) ? C[(int64_t)r * K + k] : 0.0f;
+      for (int r = 0; r < RP; ++r) v[r] = (r < R) ? C[(int64_t)r * K + k] : 0.0f;
 #pragma unroll
-    for (int r = 0; r < RP; r += 4)
-      *reinterpret_cast<float4*>(Cl + k * CP + r) = make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
-  }
-  El[min(k0, nbins - 1)] = e0;
-  for (int b = k0 + (int)blockDim.x; b < nbins; b += blockDim.x) El[b] = E_.e[b];
-  if (threadIdx.x == 0) {
-    const float nrm = sqrtf(nsq_s);
-    sc.coef = nrm > 0.0f ? lambda_s / nrm : 0.0f;
-    sc.as = adam_scalars(ad, step_s + 1);
-    if (blockIdx.x == 0) {
-      // book-keeping of spass_kernel (mode 1)
-      int pend = st->pending;
-      if (pend & QSC_PEND_C) st->step_c += 1;
-      pend &= ~QSC_PEND_C;
-      st->pending = pend | QSC_PEND_SNLL | QSC_PEND_SUPD;
-      st->normsq_s_prev = nsq_s;
-      st->iter += 1;
+      for (int r = 0; r < RP; r += 4)
+        *reinterpret_cast<float4*>(Cl + k * CP + r) = make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
     }
+    El[min(k0, nbins - 1)] = e0;
+    for (int b = k0 + (int)blockDim.x; b < nbins; b += blockDim.x) El[b] = E_.e[b];
+    STAMP(wg, 10);  // C^T rows written (its reads landed)
+    if (threadIdx.x == 0) {
+      const float nrm = sqrtf(nsq_s);
+      sc.coef = nrm > 0.0f ? lambda_s / nrm : 0.0f;
+      sc.as = adam_scalars_cached(((step_s + 1) & 1) ? ac1 : ac0, ad, step_s + 1);
+      if (blockIdx.x == 0) {
+        // book-keeping of spass_kernel (mode 1)
+        int pend = st->pending;
+        if (pend & QSC_PEND_C) st->step_c += 1;
+        pend &= ~QSC_PEND_C;
+        st->pending = pend | QSC_PEND_SNLL | QSC_PEND_SUPD;
+        st->normsq_s_prev = nsq_s;
+        st->iter += 1;
+      }
+    }
+    STAMP(wg, 11);  // (wave 0: the scalars are set)
+  };
+  if (early) {
+    slice_load(cur, s_ent, s_width, s_off, global_of(il < nsl ? il : 0), ln, S, mS, vS);
+    stage();
+  } else {
+    stage();
   }
   __syncthreads();
+  if (!early) slice_load(cur, s_ent, s_width, s_off, global_of(il < nsl ? il : 0), ln, S, mS, vS);
   STAMP(wg, 1);
   if (blockIdx.x == 0) {
     // ||C_i||^2 for the next C update's regulariser, from the staged C^T at the start (as a
@@ -1049,16 +1145,17 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
     if (threadIdx.x == 0) *cnsq = nsq;
   }
 
-  // 2. S-step over the wave's slices (next slice's reads in flight)
-  for (int n = 0; il < nsl; ++n) {
+  // 2. S-step over the wave's slices (next slice's reads in flight; the two register sets
+  //    alternate, as in spass_kernel)
+  int n = 0;
+  auto one_slice = [&](SliceIn<RP, E, ADAM>& c, SliceIn<RP, E, ADAM>& q) -> bool {
     const int il1 = local_of(n + 1);
     const bool more = il1 < nsl;
     const int s = global_of(il);
-    SliceIn<RP, E, ADAM> nxt;
-    slice_load(nxt, s_ent, s_width, s_off, more ? global_of(il1) : s, p, h, S, mS, vS);
+    slice_load(q, s_ent, s_width, s_off, more ? global_of(il1) : s, ln, S, mS, vS);
     float sv[RP];
 #pragma unroll
-    for (int r = 0; r < RP; ++r) sv[r] = cur.sv[r];
+    for (int r = 0; r < RP; ++r) sv[r] = c.sv[r];
     f2v own[RP / 2];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) own[j] = f2v{sv[2 * j], sv[2 * j + 1]} * splat2(own_scale);
@@ -1066,8 +1163,8 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_halves<RP, E, KIND, LOG>(cur.src, 2 * QSC_SLICE, cur.j1, cur.buf, own, Cl, El, lk, accp,
-                                  nll);
+    walk_halves<RP, E, KIND, LOG>(c.src, ln.ent, 2 * QSC_SLICE, c.j1, c.buf, own, Cl, El, lk,
+                                  accp, nll);
     float acc[RP];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) {
@@ -1079,23 +1176,35 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
     for (int j = 0; j < RH; ++j) {
       a[j] = pick(hmask, acc[j], acc[RH + j]);
       pv[j] = pick(hmask, sv[j], sv[RH + j]);
-      m[j] = cur.mv[j];
-      v[j] = cur.vv[j];
+      m[j] = c.mv[j];
+      v[j] = c.vv[j];
     }
     float nsq = adam_row_fast<RH>(pv, m, v, a, sc.coef, sc.as);
-    const int64_t row = ((int64_t)s * QSC_SLICE + p) * RP;
-    st_row<RH>(S + row + h * RH, pv);
-    st_row<RH>(mS + row + h * RH, m);
-    st_row<RH>(vS + row + h * RH, v);
+    const int64_t blk = (int64_t)s * QSC_SLICE * RP;  // the slice's rows (uniform)
+    st_row<RH>(S + blk, ln.half, pv);
+    st_row<RH>(mS + blk, ln.half, m);
+    st_row<RH>(vS + blk, ln.half, v);
     st_row<RH>(Sl + (il * QSC_SLICE + p) * CP + h * RH, pv);  // the tile row, for the C-pass
     nsq = wave_sum_dpp(nsq);
     if (lane == 0) part_nsq_s[s] = nsq;
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (lane == 0) part_nll_s[s] = nll_w;
-    if (!more) break;
-    cur.assign(nxt);
+    STAMP(wg, 5 + min(n, 8));  // end of the wave's n-th slice
     il = il1;
+    ++n;
+    return more;
+  };
+  if (il < nsl) {
+    SliceIn<RP, E, ADAM> nxt;
+    for (;;) {
+      if (!one_slice(cur, nxt)) break;
+      if (!one_slice(nxt, cur)) break;
+    }
   }
+
+  // the next launch's S-step scalars, by the oldest wave of block 0 (it has slack: its slices
+  // are done long before the tile barrier)
+  if (blockIdx.x == 0 && threadIdx.x == 0) adam_cache_store(acache, ad, step_s + 2);
 
   // 3. C-pass units of the tile at the new S (cpass_tile_kernel steps 1, 3, 4)
   int u = w;
@@ -1103,14 +1212,15 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
   float cv[RP];
   int wi = 0, j0 = 0, j1 = 0, k = 0;
   const V4* src = nullptr;
+  const uint32_t lo = (uint32_t)lane * (uint32_t)sizeof(V4);
   auto unit_begin = [&](int uu) {
     const int ks = uu / NP, part = uu - ks * NP;
     wi = t * nks + ks;
     const int W4 = c_width[wi] >> 2;
     j0 = (W4 * part) / NP;
     j1 = (W4 * (part + 1)) / NP;
-    src = reinterpret_cast<const V4*>(c_ent + c_off[wi]) + lane;
-    load_group(src, 64, j0, 1, max(j1 - 1, 0), buf);
+    src = reinterpret_cast<const V4*>(c_ent + c_off[wi]);
+    load_group(src, lo, 64, j0, 1, max(j1 - 1, 0), buf);
     k = c_kmap[wi * 64 + lane];  // this lane's bin (count-sorted order)
 #pragma unroll
     for (int r = 0; r < RP; ++r) cv[r] = Cl[min(k, K - 1) * CP + r];  // C_i, as the S-step used
@@ -1129,7 +1239,7 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_groups<RP, E, KIND, LOG>(src, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (NP == 1) {
 #pragma unroll
@@ -1220,7 +1330,8 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
     qsc_adam ad, float lambda_c, const float* __restrict__ normsq_ext,
     const float* __restrict__ cnsq, qsc_state* __restrict__ st,
     const float* __restrict__ part_nll_c, int npart_c, const float* __restrict__ part_nll_s,
-    const float* __restrict__ part_nsq_s, int nslices, float* __restrict__ hist, int hist_cap) {
+    const float* __restrict__ part_nsq_s, int nslices, float* __restrict__ hist, int hist_cap,
+    AdamCache* __restrict__ acache) {
   constexpr int NW = kFBlock / 64;
   __shared__ float red[NW][64];
   __shared__ Scalars sc;
@@ -1231,6 +1342,11 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
   // or the caller's global value (K-slab); never re-read here, where blocks overwrite C
   const float nsq = normsq_ext ? *normsq_ext : *cnsq;
 
+  if (blockIdx.x == R * nks + 1) {
+    // the next C-step's Adam scalars (the next S-pass settles step_c + 1 in between)
+    if (mode == 1 && threadIdx.x == 0) adam_cache_store(acache, ad, st->step_c + 2);
+    return;
+  }
   if (blockIdx.x == R * nks) {
     // book-keeping block: settle the S-pass partials (settle_s) and total the C-pass NLL.
     // Every partial is read up front (one memory round trip, batches of 8 loads in flight)
@@ -1310,9 +1426,11 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
     v0 = vC[i];
   }
   if (threadIdx.x == 0 && mode == 1) {
+    const AdamCache a0 = acache[0], a1 = acache[1];  // both slots: no dependent read on step_c
+    const int step = st->step_c + 1;
     const float nrm = sqrtf(nsq);
     sc.coef = nrm > 0.0f ? lambda_c / nrm : 0.0f;
-    sc.as = adam_scalars(ad, st->step_c + 1);
+    sc.as = adam_scalars_cached((step & 1) ? a1 : a0, ad, step);
   }
   // tile sum: wave w takes tiles w, w+16, ...; sixteen independent loads in flight per group
   const float* col = slab + (int64_t)r * Kp + k;
@@ -1477,6 +1595,7 @@ struct PassWs {
   double* init;     // 256
   int* sched;       // S-pass queue counters [kSchedQ] + finished-wave counter (zero between launches)
   float* cnsq;      // ||C||^2 of the C the last C-pass read (written by the C-pass)
+  AdamCache* acache;  // [0..1] S-side, [2..3] C-side step scalars (adam_scalars_cached)
 };
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1498,13 +1617,16 @@ PassWs carve(const qsc_obs_desc* d, int R, void* ws) {
   p.sched = (int*)w;
   w += al((kSchedQ + 1) * 4);
   p.cnsq = (float*)w;
+  w += al(4);
+  p.acache = (AdamCache*)w;
   return p;
 }
 
 size_t ws_bytes_for(const qsc_obs_desc* d, int R) {
   const int64_t Kp = (int64_t)d->nks * 64;
   return al((size_t)d->ntiles * R * Kp * 4) + al((size_t)d->ntiles * d->nks * 4) +
-         2 * al((size_t)(d->Pp / QSC_SLICE) * 4) + al(256 * 8) + al((kSchedQ + 1) * 4) + al(4);
+         2 * al((size_t)(d->Pp / QSC_SLICE) * 4) + al(256 * 8) + al((kSchedQ + 1) * 4) + al(4) +
+         al(4 * sizeof(AdamCache));
 }
 
 bool desc_ok(const qsc_obs_desc* d) {
@@ -1633,12 +1755,12 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
       hipLaunchKernelGGL((spass_kernel<RPV, ET, KD, LG, true>), grid, dim3(kSBlock), shm, s,   \
                          (const ET*)s_entries, s_width, s_off, nslices, lk, E, d->nbins, R,    \
                          d->K, d->Pp, S, C, dS, mS, vS, ad, lambda_s, st, w.snll, w.snsq,       \
-                         w.sched);                                                             \
+                         w.sched, w.acache);                                                   \
     else                                                                                       \
       hipLaunchKernelGGL((spass_kernel<RPV, ET, KD, LG, false>), grid, dim3(kSBlock), shm, s,  \
                          (const ET*)s_entries, s_width, s_off, nslices, lk, E, d->nbins, R,    \
                          d->K, d->Pp, S, C, dS, mS, vS, ad, lambda_s, st, w.snll, w.snsq,       \
-                         w.sched);                                                             \
+                         w.sched, w.acache);                                                   \
   } while (0)
   QSC_DISPATCH_PASS(SPASS_LAUNCH);
 #undef SPASS_LAUNCH
@@ -1757,7 +1879,7 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
                          dim3(threads), shm, s, (const ET*)s_entries, s_width, s_off,         \
                          (const ET*)c_entries, c_width, c_off, c_kmap, d->nks, NP, d->PT, lk, E, \
                          d->nbins, R, d->K, S, C, mS, vS, ad, lambda_s, st, w.snll, w.snsq,    \
-                         w.slab, w.cnll, w.cnsq);                                              \
+                         w.slab, w.cnll, w.cnsq, w.acache);                                    \
   } while (0)
   QSC_DISPATCH_PASS(SCPASS_LAUNCH);
 #undef SCPASS_LAUNCH
@@ -1777,10 +1899,10 @@ QSC_API int qsc_cfinish(const qsc_obs_desc* d, int32_t R, float* C, int32_t mode
   PassWs w = carve(d, R, ws);
   qsc_adam ad{};
   if (adam) ad = *adam;
-  hipLaunchKernelGGL(cfinish_kernel, dim3((unsigned)(R * d->nks + 1)), dim3(kFBlock), 0,
+  hipLaunchKernelGGL(cfinish_kernel, dim3((unsigned)(R * d->nks + 2)), dim3(kFBlock), 0,
                      STREAM(stream), w.slab, d->ntiles, d->nks, R, d->K, C, mode, dC, mC, vC, ad,
                      lambda_c, normsq_c_ext, w.cnsq, st, w.cnll, d->ntiles * d->nks, w.snll,
-                     w.snsq, d->Pp / QSC_SLICE, hist, hist_cap);
+                     w.snsq, d->Pp / QSC_SLICE, hist, hist_cap, w.acache + 2);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }

@@ -1,14 +1,14 @@
 #!/bin/bash
-# A/B: default build vs a variant library (bench value + fused kernel time), alternating
+# A/B: default build vs variant libraries (bench value, fused kernel time, C-finish time),
+# alternating, REPS rounds:  REPS=3 bash tools/gpu_ab.sh variants/libqsc_a.so variants/libqsc_b.so
 mkdir -p gpurun_out
-V=${1:-variants/libqsc_noprio.so}
-for rep in 1 2 3; do
-  for lib in default $V; do
+for rep in $(seq ${REPS:-3}); do
+  for lib in default "$@"; do
     if [ $lib = default ]; then
-      timeout -k 10 200 python bench.py --cpu-baseline 0 > gpurun_out/ab.log 2>&1 || exit $?
+      timeout -k 10 200 python bench.py --cpu-baseline 0 ${BENCH_ARGS} > gpurun_out/ab.log 2>&1 || exit $?
     else
-      QSC_LIB_PATH=$lib timeout -k 10 200 python bench.py --cpu-baseline 0 > gpurun_out/ab.log 2>&1 || exit $?
+      QSC_LIB_PATH=$lib timeout -k 10 200 python bench.py --cpu-baseline 0 ${BENCH_ARGS} > gpurun_out/ab.log 2>&1 || exit $?
     fi
-    tail -1 gpurun_out/ab.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$lib', round(d['value']), round(d['kernels']['scfused_us'] or 0, 2), round(d['kernels']['cfinish_us'], 2))"
+    tail -1 gpurun_out/ab.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('%-32s' % '$lib', round(d['value']), round(d['kernels']['scfused_us'] or 0, 2), round(d['kernels']['cfinish_us'], 2))"
   done
 done
