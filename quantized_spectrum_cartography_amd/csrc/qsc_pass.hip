@@ -41,7 +41,23 @@ constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 #endif
 // fused launch: waves that read their first slice before the staging barrier (see scfused)
 #ifndef QSC_EARLY_WAVES
-#define QSC_EARLY_WAVES 16
+#define QSC_EARLY_WAVES 4
+#endif
+// fused launch: a wave's first slice lands before its second slice's reads are issued
+#ifndef QSC_FIRST_WAIT
+#define QSC_FIRST_WAIT 1
+#endif
+// software-pipelined LDS gathers in the C-pass walk (walk_groups).  (The same in the S-pass
+// walk spills at the 128-VGPR budget of the fused launch and was slower: DESIGN.md 7b.)
+#ifndef QSC_ROW_PF_C
+#define QSC_ROW_PF_C 1
+#endif
+// fused launch: C^T staged from 16-B reads; part-sum bins read at the start
+#ifndef QSC_CT_VEC
+#define QSC_CT_VEC 1
+#endif
+#ifndef QSC_KMAP_PF
+#define QSC_KMAP_PF 1
 #endif
 #ifndef QSC_CPASS_WAVES
 #define QSC_CPASS_WAVES 4
@@ -169,26 +185,51 @@ struct Scalars {
 // the entry's low bits.  Pad entries carry index 0 (a valid row) and code kPad; the one-bit kind
 // moves them to z' = kPadZ where they contribute exactly 0, the other kinds mask them.  The NLL
 // is accumulated as a pair (summed by the caller).
+// the LDS rows of an entry pair (the gather half of pair_step)
+template <int RP, typename E>
+__device__ __forceinline__ void pair_rows(uint32_t ea, uint32_t eb, const f2v (&own)[RP / 2],
+                                          const float* __restrict__ tab, f2v (&oa)[RP / 2],
+                                          f2v (&ob)[RP / 2]) {
+  using T = Ent<E>;
+#if QSC_DIAG_NOLDS  // diagnostic build: no gather (bounds the LDS share of the pass)
+#pragma unroll
+  for (int j = 0; j < RP / 2; ++j) {
+    oa[j] = own[j] + splat2((float)(ea & T::kMask));
+    ob[j] = own[j] + splat2((float)(eb & T::kMask));
+  }
+#else
+  (void)own;
+  lds_row2<RP>(tab + (ea & T::kMask) * Pitch<RP>::v, oa);
+  lds_row2<RP>(tab + (eb & T::kMask) * Pitch<RP>::v, ob);
+#endif
+}
+
+// the arithmetic half of pair_step on already gathered rows oa, ob
+template <int RP, typename E, int KIND, bool LOG>
+__device__ __forceinline__ void pair_math(uint32_t ea, uint32_t eb, const f2v (&own)[RP / 2],
+                                          const f2v (&oa)[RP / 2], const f2v (&ob)[RP / 2],
+                                          const float2* __restrict__ edges, const Lik& lk,
+                                          f2v (&acc)[RP / 2], f2v& nll, bool valid);
+
 template <int RP, typename E, int KIND, bool LOG>
 __device__ __forceinline__ void pair_step(uint32_t ea, uint32_t eb, const f2v (&own)[RP / 2],
                                           const float* __restrict__ tab,
+                                          const float2* __restrict__ edges, const Lik& lk,
+                                          f2v (&acc)[RP / 2], f2v& nll, bool valid) {
+  f2v oa[RP / 2], ob[RP / 2];
+  pair_rows<RP, E>(ea, eb, own, tab, oa, ob);
+  pair_math<RP, E, KIND, LOG>(ea, eb, own, oa, ob, edges, lk, acc, nll, valid);
+}
+
+template <int RP, typename E, int KIND, bool LOG>
+__device__ __forceinline__ void pair_math(uint32_t ea, uint32_t eb, const f2v (&own)[RP / 2],
+                                          const f2v (&oa)[RP / 2], const f2v (&ob)[RP / 2],
                                           const float2* __restrict__ edges, const Lik& lk,
                                           f2v (&acc)[RP / 2], f2v& nll, bool valid) {
   using T = Ent<E>;
   {
     const int ca = (int)(ea >> T::kBits), cb = (int)(eb >> T::kBits);
     const bool pa = (ca == T::kPad) || !valid, pb = (cb == T::kPad) || !valid;
-    f2v oa[RP / 2], ob[RP / 2];
-#if QSC_DIAG_NOLDS  // diagnostic build: no gather (bounds the LDS share of the pass)
-#pragma unroll
-    for (int j = 0; j < RP / 2; ++j) {
-      oa[j] = own[j] + splat2((float)(ea & T::kMask));
-      ob[j] = own[j] + splat2((float)(eb & T::kMask));
-    }
-#else
-    lds_row2<RP>(tab + (ea & T::kMask) * Pitch<RP>::v, oa);
-    lds_row2<RP>(tab + (eb & T::kMask) * Pitch<RP>::v, ob);
-#endif
     f2v t;
     if constexpr (KIND == LIK_ONEBIT)
       t = f2v{dot2z<RP>(own, oa, lk.ob_thr), dot2z<RP>(own, ob, lk.ob_thr)};
@@ -272,17 +313,54 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
                                             f2v (&acc)[RP / 2], f2v& nll) {
   using V4 = typename Ent<E>::V4;
   const int jlast = max(j1 - 1, 0);
+#if QSC_ROW_PF_C
+  // software-pipelined gather: the LDS rows of the next entry pair are read before the current
+  // pair's arithmetic, so the LDS latency runs under it (the group's chunks are loaded, clamped,
+  // so a prefetch past the list end reads valid rows that are never used)
+  f2v ra[RP / 2], rb[RP / 2];
+  {
+    uint32_t e[4];
+    Ent<E>::unpack(b[0], e);
+    pair_rows<RP, E>(e[0], e[1], own, tab, ra, rb);
+  }
+#endif
   for (;;) {
     const int jn = jb + kGroup * js;
     const bool more = jn < j1;
     V4 nb[kGroup];
     load_group(src, lo, row, jn, js, jlast, nb);  // unconditional: static vmcnt accounting
+#if QSC_ROW_PF_C
+#pragma unroll
+    for (int i = 0; i < kGroup; ++i)
+      if (jb + i * js < j1) {
+        uint32_t e[4];
+        Ent<E>::unpack(b[i], e);
+        f2v xa[RP / 2], xb[RP / 2];
+        pair_rows<RP, E>(e[2], e[3], own, tab, xa, xb);
+        pair_math<RP, E, KIND, LOG>(e[0], e[1], own, ra, rb, edges, lk, acc, nll, true);
+        if (i + 1 < kGroup) {
+          uint32_t f[4];
+          Ent<E>::unpack(b[i + 1], f);
+          pair_rows<RP, E>(f[0], f[1], own, tab, ra, rb);
+        }
+        pair_math<RP, E, KIND, LOG>(e[2], e[3], own, xa, xb, edges, lk, acc, nll, true);
+      }
+    if (!more) break;
+#pragma unroll
+    for (int i = 0; i < kGroup; ++i) b[i] = nb[i];
+    {
+      uint32_t e[4];
+      Ent<E>::unpack(b[0], e);
+      pair_rows<RP, E>(e[0], e[1], own, tab, ra, rb);
+    }
+#else
 #pragma unroll
     for (int i = 0; i < kGroup; ++i)
       if (jb + i * js < j1) chunk<RP, E, KIND, LOG>(b[i], own, tab, edges, lk, acc, nll);
     if (!more) break;
 #pragma unroll
     for (int i = 0; i < kGroup; ++i) b[i] = nb[i];
+#endif
     jb = jn;
   }
 }
@@ -1011,7 +1089,7 @@ size_t cpass_tile_lds(int PT, int R, int nks, int NP) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Fused S-step + next C-pass, one workgroup per C-pass pixel tile (RP <= 8, 16 waves).
+// Fused S-step + next C-pass, one workgroup per C-pass pixel tile (16 waves; 8 at rank 16).
 // The tile's whole position slices (tile_pos) get their S-step first -- likelihood, dS and
 // Adam exactly as spass_kernel, wave w taking the tile's slices w, 2*16-1-w, ... (snake over
 // the count-sorted slices) -- and the new S rows are written to HBM (S, mS, vS) AND into the
@@ -1022,8 +1100,15 @@ size_t cpass_tile_lds(int PT, int R, int nks, int NP) {
 // Kernel sequence semantics are unchanged: spass_i then cpass_{i+1} (same partials, same
 // state protocol), so a solver runs cpass+cfinish, then (fused + cfinish) x (n-1), then spass.
 // ---------------------------------------------------------------------------------------
+// fused launch block: 16 waves (4 per SIMD, 128 VGPRs) up to rank 8; 8 waves at rank 16, whose
+// two slice register sets and 16-float rows need up to 256 VGPRs (2 waves per SIMD)
+template <int RP>
+struct FusedBlock {
+  static constexpr int v = RP > 8 ? 512 : 1024;
+};
+
 template <int RP, typename E, int KIND, bool LOG>
-__global__ void __launch_bounds__(kCTBlock) scfused_kernel(
+__global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
     const E* __restrict__ s_ent, const int* __restrict__ s_width, const int64_t* __restrict__ s_off,
     const E* __restrict__ c_ent, const int* __restrict__ c_width, const int64_t* __restrict__ c_off,
     const int* __restrict__ c_kmap, int nks, int NP, int PT, Lik lk, Edges E_, int nbins, int R,
@@ -1055,7 +1140,7 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
   // this wave's n-th slice of the tile (local index) and its global slice
   auto local_of = [&](int n) { return n * NW + ((n & 1) ? (NW - 1 - w) : w); };
   auto global_of = [&](int i) { return i * nt + ((i & 1) ? (nt - 1 - t) : t); };
-  [[maybe_unused]] const int wg = blockIdx.x * (kCTBlock / 64) + w;  // (diagnostic stamps)
+  [[maybe_unused]] const int wg = blockIdx.x * (FusedBlock<RP>::v / 64) + w;  // (stamps)
   STAMP(wg, 0);
   RSTAMP(wg, 28);
 #if QSC_DIAG_STAMPS
@@ -1065,10 +1150,38 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
   // 1. C^T / edge / state reads first (the LDS staging then waits only for them: vmcnt
   //    retires in issue order), then the first slice's reads, then the staging
   const int k0 = threadIdx.x;
+#if QSC_CT_VEC
+  // C^T from 16-B reads of the [R][K] C: thread i holds C's flat floats 4i..4i+3 (one row r,
+  // four consecutive bins) and writes them transposed; 32x fewer read instructions than a
+  // float per (thread, row)
+  const int n4 = (R * K) >> 2;
+  const bool cvec = (K & 3) == 0 && ((reinterpret_cast<uintptr_t>(C) & 15) == 0);
+  float4 cq = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  float c0[RP];
+  if (cvec) {
+    cq = reinterpret_cast<const float4*>(C)[min(k0, n4 - 1)];
+  } else {
+#pragma unroll
+    for (int r = 0; r < RP; ++r) c0[r] = C[(int64_t)min(r, R - 1) * K + min(k0, K - 1)];
+  }
+#else
   float c0[RP];
 #pragma unroll
   for (int r = 0; r < RP; ++r) c0[r] = C[(int64_t)min(r, R - 1) * K + min(k0, K - 1)];
+#endif
   const float2 e0 = E_.e[min(k0, nbins - 1)];
+#if QSC_KMAP_PF
+  // the bins of this thread's first two part-sum outputs (step 4), read now: at the tail they
+  // would be a dependent global read after the last unit
+  const int nps = nks * R * 64;
+  int km_pf[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = min(k0 + j * (int)blockDim.x, nps - 1);
+    const int ks = i / (R * 64), l = (i - ks * (R * 64)) & 63;
+    km_pf[j] = c_kmap[((int64_t)t * nks + ks) * 64 + l];
+  }
+#endif
   float nsq_s = 0.0f;
   int step_s = 0;
   AdamCache ac0{}, ac1{};
@@ -1088,19 +1201,40 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
   // burst is then a quarter of the tile's slice data and the S-step starts that much earlier.
   const bool early = w < QSC_EARLY_WAVES;
   auto stage = [&]() {
-    const int kw = min(k0, K - 1);  // branch-free: threads past K rewrite row K-1
-#pragma unroll
-    for (int r = 0; r < RP; r += 4)
-      *reinterpret_cast<float4*>(Cl + kw * CP + r) =
-          make_float4(r < R ? c0[r] : 0.0f, r + 1 < R ? c0[r + 1] : 0.0f,
-                      r + 2 < R ? c0[r + 2] : 0.0f, r + 3 < R ? c0[r + 3] : 0.0f);
-    for (int k = k0 + (int)blockDim.x; k < K; k += blockDim.x) {
-      float v[RP];
-#pragma unroll
-      for (int r = 0; r < RP; ++r) v[r] = (r < R) ? C[(int64_t)r * K + k] : 0.0f;
+#if QSC_CT_VEC
+    if (cvec) {
+      auto put = [&](int i, const float4& v) {
+        const int f = 4 * i, r = f / K, k = f - r * K;
+        Cl[k * CP + r] = v.x;
+        Cl[(k + 1) * CP + r] = v.y;
+        Cl[(k + 2) * CP + r] = v.z;
+        Cl[(k + 3) * CP + r] = v.w;
+      };
+      if (k0 < n4) put(k0, cq);
+      for (int i = k0 + (int)blockDim.x; i < n4; i += blockDim.x)
+        put(i, reinterpret_cast<const float4*>(C)[i]);
+      for (int i = k0; i < K * (RP - R); i += blockDim.x) {  // rows R..RP-1 are zero
+        const int k = i / (RP - R), r = R + (i - k * (RP - R));
+        Cl[k * CP + r] = 0.0f;
+      }
+    } else
+#endif
+    {
+      const int kw = min(k0, K - 1);  // branch-free: threads past K rewrite row K-1
 #pragma unroll
       for (int r = 0; r < RP; r += 4)
-        *reinterpret_cast<float4*>(Cl + k * CP + r) = make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
+        *reinterpret_cast<float4*>(Cl + kw * CP + r) =
+            make_float4(r < R ? c0[r] : 0.0f, r + 1 < R ? c0[r + 1] : 0.0f,
+                        r + 2 < R ? c0[r + 2] : 0.0f, r + 3 < R ? c0[r + 3] : 0.0f);
+      for (int k = k0 + (int)blockDim.x; k < K; k += blockDim.x) {
+        float v[RP];
+#pragma unroll
+        for (int r = 0; r < RP; ++r) v[r] = (r < R) ? C[(int64_t)r * K + k] : 0.0f;
+#pragma unroll
+        for (int r = 0; r < RP; r += 4)
+          *reinterpret_cast<float4*>(Cl + k * CP + r) =
+              make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
+      }
     }
     El[min(k0, nbins - 1)] = e0;
     for (int b = k0 + (int)blockDim.x; b < nbins; b += blockDim.x) El[b] = E_.e[b];
@@ -1152,6 +1286,14 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
     const int il1 = local_of(n + 1);
     const bool more = il1 < nsl;
     const int s = global_of(il);
+#if QSC_FIRST_WAIT
+    // the first slice's reads land before the second slice's are issued: the launch's first
+    // burst is then one slice per wave, not two
+    if (n == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      STAMP(wg, 12);
+    }
+#endif
     slice_load(q, s_ent, s_width, s_off, more ? global_of(il1) : s, ln, S, mS, vS);
     float sv[RP];
 #pragma unroll
@@ -1261,13 +1403,18 @@ __global__ void __launch_bounds__(kCTBlock) scfused_kernel(
   STAMP(wg, 4);
   if (NP > 1) {
     __syncthreads();
-    for (int i = threadIdx.x; i < nks * R * 64; i += blockDim.x) {
+    for (int i = threadIdx.x, j = 0; i < nks * R * 64; i += blockDim.x, ++j) {
       const int ks = i / (R * 64), rl = i - ks * (R * 64);
       const float* pp0 = Pl + (size_t)ks * NP * R * 64 + rl;
       float acc = pp0[0];
       for (int pp = 1; pp < NP; ++pp) acc += pp0[(size_t)pp * R * 64];
       const int r = rl >> 6, l = rl & 63;
-      slab[((int64_t)t * R + r) * Kp + c_kmap[((int64_t)t * nks + ks) * 64 + l]] = acc;
+#if QSC_KMAP_PF
+      const int kk = j == 0 ? km_pf[0] : j == 1 ? km_pf[1] : c_kmap[((int64_t)t * nks + ks) * 64 + l];
+#else
+      const int kk = c_kmap[((int64_t)t * nks + ks) * 64 + l];
+#endif
+      slab[((int64_t)t * R + r) * Kp + kk] = acc;
     }
     for (int ks = threadIdx.x; ks < nks; ks += blockDim.x) {
       float acc = Nl[ks * NP];
@@ -1836,7 +1983,7 @@ static int cpass_parts(const qsc_obs_desc* d) {
 }
 
 QSC_API int qsc_scpass_supported(const qsc_obs_desc* d, int32_t R) {
-  if (!desc_ok(d) || R < 1 || R > 8) return 0;
+  if (!desc_ok(d) || R < 1 || R > 16) return 0;
   const int NP = cpass_parts(d);
   const int U = d->nks * NP;
   return (U >= 4 && U <= QSC_CTILE_MAXW && d->PT <= 4096 &&
@@ -1868,13 +2015,13 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
   else if (!m->log_model)
     scale_edges(&E, m->nbounds - 1, lk.a);
   const qsc_adam ad = *adam;
-  // waves: two S-step slices each (the tile's nsl slices), 4..16
+  // waves: two S-step slices each (the tile's nsl slices), 4..16 (4..8 at rank 16)
   const int nsl = d->PT / QSC_SLICE;
-  const unsigned threads = 64u * (unsigned)std::min(16, std::max(4, nsl / 2));
+  const unsigned threads =
+      64u * (unsigned)std::min(RP > 8 ? 8 : 16, std::max(4, nsl / 2));
   hipStream_t s = STREAM(stream);
 #define SCPASS_LAUNCH(RPV, ET, KD, LG)                                                         \
   do {                                                                                         \
-    if constexpr (RPV <= 8)                                                                    \
       hipLaunchKernelGGL((scfused_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles),         \
                          dim3(threads), shm, s, (const ET*)s_entries, s_width, s_off,         \
                          (const ET*)c_entries, c_width, c_off, c_kmap, d->nks, NP, d->PT, lk, E, \

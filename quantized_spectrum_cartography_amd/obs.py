@@ -28,6 +28,14 @@ def default_tile(P, R, K):
     t = 128
     while t * 2 <= want and t < 1024:
         t *= 2
+    if R > 8:
+        # rank 16: the fused S-step + C-pass launch holds C^T and the S tile at a 20-float
+        # pitch in LDS (scfused_lds, qsc_pass.hip); halve the tile until both fit, with the
+        # part-sum area of the largest part count it may use
+        parts = 1 if nks >= 16 else 16 // nks
+        part_sum = 16 * 64 * 4 * nks * parts if parts > 1 else 0
+        while t > 128 and 32 + K * 80 + 2048 + t * 80 + part_sum + 64 > 160 * 1024:
+            t //= 2
     return t
 
 

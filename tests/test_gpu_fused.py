@@ -148,7 +148,11 @@ def test_solver_graph_replay_matches_eager():
                           (44, 5, 64, 64, 64, False, "squared", 2, 512),
                           (46, 4, 64, 64, 64, True, "probit", 2, 512),
                           (47, 6, 40, 56, 100, False, "probit", 20, 256),  # wide (uint32) entries
-                          (48, 1, 33, 31, 70, False, "probit", 2, 256)])   # R = 1, ragged P, K
+                          (48, 1, 33, 31, 70, False, "probit", 2, 256),    # R = 1, ragged P, K
+                          # rank 16 (8-wave launch, 20-float LDS pitch), R = 12 padded to 16
+                          (49, 16, 64, 64, 256, False, "probit", 2, 512),
+                          (50, 12, 48, 64, 192, False, "squared", 2, 256),
+                          (51, 16, 64, 64, 128, True, "probit", 2, 512)])
 def test_fused_spass_cpass_bitexact(seed, R, I, J, K, log_model, loss, nbins, tile):
     """qsc_scpass (S-step + next C-pass in one launch) reproduces spass + cpass bit for bit:
     S, C and the cost history after n iterations, eager and hipGraph."""

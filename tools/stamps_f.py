@@ -50,6 +50,9 @@ def main():
     print("  start      ", pu(st[:, 28] - r0))
     print("  end        ", pu(st[:, 29] - r0))
     print("  staging    ", pc(st[:, 1] - st[:, 0]))
+    if (st[:, 12] > 0).any():
+        m = st[:, 12] > 0
+        print("  1st data   ", pc(st[m, 12] - st[m, 1]))
     print("  S-step     ", pc(st[:, 2] - st[:, 1]))
     print("  tile wait  ", pc(st[:, 3] - st[:, 2]))
     print("  C units    ", pc(st[:, 4] - st[:, 3]))

@@ -48,9 +48,10 @@ def main():
             for sm in range(4):
                 ws = w[simd[w] == sm]
                 for x in ws:
-                    sl = [us(st[x, j] - t0) for j in range(5, 8) if st[x, j] > 0]
-                    print("  simd %d wave %2d: staged %5.2f slices %s S-end %5.2f C %5.2f-%5.2f end %5.2f" % (
-                        sm, x - blk * 16, us(st[x, 1] - t0), " ".join("%5.2f" % v for v in sl),
+                    sl = [us(st[x, j] - t0) for j in range(5, 8) if 0 < st[x, j] - t0 < 10 ** 7]
+                    fd = us(st[x, 12] - t0) if st[x, 12] > 0 else float("nan")
+                    print("  simd %d wave %2d: staged %5.2f data %5.2f slices %s S-end %5.2f C %5.2f-%5.2f end %5.2f" % (
+                        sm, x - blk * 16, us(st[x, 1] - t0), fd, " ".join("%5.2f" % v for v in sl),
                         us(st[x, 2] - t0), us(st[x, 3] - t0), us(st[x, 4] - t0), us(st[x, 31] - t0)))
     t0b = np.array([st[b * 16:(b + 1) * 16, 0].min() for b in range(256)]).repeat(16)
     for name, j in (("C^T written", 10), ("scalars set", 11), ("barrier", 1)):
