@@ -129,7 +129,13 @@ typedef struct qsc_state {
  *     is position  g*QSC_SLICE + qlocal%QSC_SLICE,  g = i*ntiles + (i odd ? ntiles-1-t : t),
  *     i = qlocal/QSC_SLICE.
  *  narrow (wide == 0): uint16 entries, KBITS = QBITS = 12, code PAD = 15 (K, PT <= 4096, nbins <= 15)
- *  wide   (wide == 1): uint32 entries, KBITS = QBITS = 24, code PAD = 255 */
+ *  wide   (wide == 1): uint32 entries, KBITS = QBITS = 24, code PAD = 255
+ *  Signed-row entries (rowfmt == 1; one-bit linear model, narrow only, set by the caller between
+ *  qsc_obs_layout and qsc_obs_fill when qsc_obs_signed_rows_ok): the value is the row of the
+ *  pass's LDS table directly -- S-format  k + (code == 1 ? K : 0),  pad 2K;  C-format
+ *  qlocal + (code == 1 ? PT : 0),  pad 2PT.  The passes stage each factor row twice, as
+ *  [+row, +thr'] and [-row, -thr'] (thr' the scaled threshold), plus a neutral pad row, so an
+ *  entry's code is applied by the gather itself (z of code 1 is -z of code 0, exactly). */
 typedef struct qsc_obs_desc {
   int32_t K;      /* frequency bins in this (local) slab */
   int32_t P;      /* pixels I*J */
@@ -142,6 +148,8 @@ typedef struct qsc_obs_desc {
   int64_t nnz;    /* observed entries */
   int64_t s_entries; /* S-format entries incl. padding */
   int64_t c_entries; /* C-format entries incl. padding */
+  int32_t rowfmt; /* 0: code-field entries; 1: signed-row entries (see above) */
+  int32_t reserved_;
 } qsc_obs_desc;
 
 /* ---------------------------------------------------------------------------------------
@@ -239,6 +247,11 @@ QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t P
                            const int32_t* perm, const int32_t* cnt, int32_t* s_width,
                            int64_t* s_off, int32_t* c_width, int64_t* c_off, int32_t* c_kmap,
                            void* ws, size_t ws_bytes, qsc_obs_desc* desc, void* stream);
+/* 1 if the signed-row entry format (rowfmt = 1) applies to this layout at rank R under model m:
+ * the one-bit linear model (saturated outer edges, probit loss), narrow entries, and the doubled
+ * LDS tables of every pass fit.  Passes given a rowfmt = 1 layout they cannot run return
+ * QSC_EINVAL. */
+QSC_API int qsc_obs_signed_rows_ok(const qsc_obs_desc* desc, int32_t R, const qsc_model* m);
 QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* desc, const int32_t* perm,
                          const int32_t* s_width, const int64_t* s_off, const int32_t* c_width,
                          const int64_t* c_off, const int32_t* c_kmap, void* s_entries,

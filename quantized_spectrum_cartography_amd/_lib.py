@@ -41,7 +41,8 @@ class QscObsDesc(ctypes.Structure):
     _fields_ = [("K", ctypes.c_int32), ("P", ctypes.c_int32), ("Pp", ctypes.c_int32),
                 ("PT", ctypes.c_int32), ("ntiles", ctypes.c_int32), ("nks", ctypes.c_int32),
                 ("wide", ctypes.c_int32), ("nbins", ctypes.c_int32), ("nnz", ctypes.c_int64),
-                ("s_entries", ctypes.c_int64), ("c_entries", ctypes.c_int64)]
+                ("s_entries", ctypes.c_int64), ("c_entries", ctypes.c_int64),
+                ("rowfmt", ctypes.c_int32), ("reserved_", ctypes.c_int32)]
 
 
 # device-resident qsc_state: 4 int32 + 5 float + 7 reserved float

@@ -193,6 +193,7 @@ struct Lik {
   float ob_scale; // fp32(sqrt(log2 e) / a): the factor rows are pre-scaled by -ob_scale
   float ob_thr;   // fp32(thr * sqrt(log2 e) / a)
   float ob_kg;    // fp32(kgrad / kMillsK)
+  int th_off;     // signed-row kind: float offset of the gather table's threshold column
 };
 
 // one-bit Mills-ratio form.  With c = sqrt(log2 e) and u = c |z|, the probit tail
@@ -228,6 +229,7 @@ inline Lik make_lik(const qsc_model* m) {
   l.ob_scale = (float)(c / (double)l.a);
   l.ob_thr = (float)((double)l.thr * c / (double)l.a);
   l.ob_kg = (float)((double)p.kgrad / kMillsK);
+  l.th_off = 0;
 #if QSC_FTZ_SAT
   l.ob_kg = (float)((double)p.kgrad / kMillsK * 0x1p101);  // E is carried 2^-101 low
 #endif
@@ -237,7 +239,10 @@ inline Lik make_lik(const qsc_model* m) {
 // Fused-pass likelihood kinds: one active edge (linear one-bit with saturated +-1e5 outer
 // edges: P = F(thr - x) for code 0, 1 - F(thr - x) for code 1, exactly the reference's values),
 // or the general two-edge form (multi-bin and/or log model).
-enum { LIK_ONEBIT = 0, LIK_GENERAL = 1, LIK_SQUARED = 2 };
+// LIK_ONEBIT_SR: the one-bit kind on signed-row layouts (qsc_obs_desc::rowfmt 1): the gathered
+// row carries the entry's sign and threshold, [s*row, s*thr'] (s = +1 for code 0, -1 for code 1,
+// pad rows [0, kPadZ]), so the walk evaluates z~ = s*z' with no code, pad or sign handling.
+enum { LIK_ONEBIT = 0, LIK_GENERAL = 1, LIK_SQUARED = 2, LIK_ONEBIT_SR = 3 };
 
 inline int lik_kind(const qsc_model* m) {
   if (m->loss == QSC_LOSS_SQUARED) return LIK_SQUARED;
@@ -337,6 +342,40 @@ __device__ __forceinline__ void lik_grad2(f2v t, int c0, int c1, bool pa, bool p
     const f2v r = x - f2v{e0.x, e1.x};
     g = splat2(2.0f) * r * tinv;
     log2P = -(r * r) * splat2(kInvLn2);
+  } else if (KIND == LIK_ONEBIT_SR) {
+    // z~ = s z' (the sign folded into the gathered row): the tail side is z~ < 0 for both codes
+    // (code 0: z' < 0; code 1: z' > 0) and g needs no sign flip, the row being s*row.  Same
+    // arithmetic as the one-bit kind below, so the same bits (but for z' == 0 exactly, where
+    // T and 1 - T are both 1/2 to within the fit's 3e-7)
+    const f2v z = t;
+    const f2v u = f2v{__builtin_fabsf(z.x), __builtin_fabsf(z.y)};
+#if QSC_FTZ_SAT
+    const f2v E = exp2_2(fma2(-z, z, splat2(kMillsLogK - 101.0f)));
+#else
+    const f2v E = exp2_2(fma2(-z, z, splat2(kMillsLogK)));
+#endif
+    f2v N = u + splat2(kMillsN2);
+    N = fma2(N, u, splat2(kMillsN1));
+    N = fma2(N, u, splat2(kMillsN0));
+    f2v D = u + splat2(kMillsD3);
+    D = fma2(D, u, splat2(kMillsD2));
+    D = fma2(D, u, splat2(kMillsD1));
+    D = fma2(D, u, splat2(kMillsD0));
+#if QSC_FTZ_SAT
+    const f2v Ts = ((E * N) * rcp2(D)) * splat2(0x1p101f);
+#else
+    const f2v T = (E * N) * rcp2(D);
+    const f2v Ts = f2v{T.x < kMillsTsat ? 0.0f : T.x, T.y < kMillsTsat ? 0.0f : T.y};
+#endif
+    const f2v Q = splat2(1.0f) - Ts;
+    const f2v P = f2v{z.x < 0.0f ? Ts.x : Q.x, z.y < 0.0f ? Ts.y : Q.y};
+    g = (E * splat2(c.ob_kg)) * rcp2(P);
+    log2P = log2_2(P);
+    (void)c0;
+    (void)c1;
+    (void)pa;
+    (void)pb;
+    (void)edges;
   } else if (KIND == LIK_ONEBIT) {
     f2v z = t;
     if (pa) z.x = kPadZ;

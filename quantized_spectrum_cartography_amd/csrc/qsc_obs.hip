@@ -114,11 +114,25 @@ __device__ __forceinline__ int64_t slot(int64_t base, int lanes, int lane, int j
   return base + (int64_t)(j >> 2) * (lanes * 4) + lane * 4 + (j & 3);
 }
 
+// Entry values (include/qsc.h): code-field form  idx | code << KBITS  (pad: code PAD), or the
+// signed-row form (rowfmt 1)  idx + (code == 1 ? rows : 0)  (pad: row 2 * rows), where `rows` is
+// the table's row count, K for the S-format and PT for the C-format
+template <typename E>
+__device__ __forceinline__ E entry_of(uint32_t idx, uint32_t code, int sr, int rows) {
+  using Tr = EntryTraits<E>;
+  return sr ? (E)(idx + (code == 1 ? (uint32_t)rows : 0u)) : (E)(idx | (code << Tr::kBits));
+}
+template <typename E>
+__device__ __forceinline__ E pad_of(int sr, int rows) {
+  using Tr = EntryTraits<E>;
+  return sr ? (E)(2u * (uint32_t)rows) : (E)(Tr::kPad << Tr::kBits);
+}
+
 // pad entries after the last list (read-ahead tail, QSC_ENTRY_TAIL)
 template <typename E>
-__global__ void tail_fill_kernel(E* __restrict__ ent, int64_t start, int n) {
+__global__ void tail_fill_kernel(E* __restrict__ ent, int64_t start, int n, int sr, int rows) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) ent[start + i] = (E)(EntryTraits<E>::kPad << EntryTraits<E>::kBits);
+  if (i < n) ent[start + i] = pad_of<E>(sr, rows);
 }
 
 template <typename E>
@@ -127,8 +141,7 @@ __global__ void __launch_bounds__(kBlock) s_fill_kernel(const uint8_t* __restric
                                                         int P, int Pp,
                                                         const int* __restrict__ width,
                                                         const int64_t* __restrict__ off,
-                                                        E* __restrict__ ent) {
-  using Tr = EntryTraits<E>;
+                                                        E* __restrict__ ent, int sr) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= Pp) return;
   const int s = q / QSC_SLICE, lane = q % QSC_SLICE;
@@ -140,10 +153,10 @@ __global__ void __launch_bounds__(kBlock) s_fill_kernel(const uint8_t* __restric
     for (int k = 0; k < K; ++k) {
       const uint8_t c = codes[(int64_t)k * P + p];
       if (c != QSC_UNOBSERVED)
-        ent[slot(base, QSC_SLICE, lane, j++)] = (E)((uint32_t)k | ((uint32_t)c << Tr::kBits));
+        ent[slot(base, QSC_SLICE, lane, j++)] = entry_of<E>((uint32_t)k, c, sr, K);
     }
   }
-  for (; j < W; ++j) ent[slot(base, QSC_SLICE, lane, j)] = (E)(Tr::kPad << Tr::kBits);
+  for (; j < W; ++j) ent[slot(base, QSC_SLICE, lane, j)] = pad_of<E>(sr, K);
 }
 
 template <typename E>
@@ -153,8 +166,7 @@ __global__ void __launch_bounds__(kBlock) c_fill_kernel(const uint8_t* __restric
                                                         const int* __restrict__ width,
                                                         const int64_t* __restrict__ off,
                                                         const int* __restrict__ kmap,
-                                                        E* __restrict__ ent) {
-  using Tr = EntryTraits<E>;
+                                                        E* __restrict__ ent, int sr) {
   const int t = blockIdx.x;
   for (int kk = threadIdx.x; kk < nks * 64; kk += blockDim.x) {
     const int ks = kk >> 6, lane = kk & 63;
@@ -169,10 +181,10 @@ __global__ void __launch_bounds__(kBlock) c_fill_kernel(const uint8_t* __restric
         if (p < 0 || p >= P) continue;
         const uint8_t c = codes[(int64_t)k * P + p];
         if (c != QSC_UNOBSERVED)
-          ent[slot(base, 64, lane, j++)] = (E)((uint32_t)ql | ((uint32_t)c << Tr::kBits));
+          ent[slot(base, 64, lane, j++)] = entry_of<E>((uint32_t)ql, c, sr, PT);
       }
     }
-    for (; j < W; ++j) ent[slot(base, 64, lane, j)] = (E)(Tr::kPad << Tr::kBits);
+    for (; j < W; ++j) ent[slot(base, 64, lane, j)] = pad_of<E>(sr, PT);
   }
 }
 
@@ -313,6 +325,8 @@ QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t P
   desc->s_entries = host_tot[0] + QSC_ENTRY_TAIL;
   desc->c_entries = host_tot[1] + QSC_ENTRY_TAIL;
   desc->nnz = host_tot[2];
+  desc->rowfmt = 0;
+  desc->reserved_ = 0;
   return QSC_OK;
 }
 
@@ -323,32 +337,37 @@ QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* d, const int3
   if (!d || !codes || !perm || !s_width || !s_off || !c_width || !c_off || !c_kmap ||
       !s_entries || !c_entries || d->s_entries < QSC_ENTRY_TAIL || d->c_entries < QSC_ENTRY_TAIL)
     return QSC_EINVAL;
+  // signed rows: narrow entries, every row index (2K, 2PT) representable
+  const int sr = d->rowfmt == 1 ? 1 : 0;
+  if (d->rowfmt != 0 && (d->rowfmt != 1 || d->wide || 2 * (int64_t)d->K > 0xFFFF ||
+                         2 * (int64_t)d->PT > 0xFFFF || d->nbins != 2))
+    return QSC_EINVAL;
   hipStream_t s = STREAM(stream);
   const dim3 tg((QSC_ENTRY_TAIL + kBlock - 1) / kBlock), tb(kBlock);
   if (d->wide) {
     hipLaunchKernelGGL(tail_fill_kernel<uint32_t>, tg, tb, 0, s, (uint32_t*)s_entries,
-                       d->s_entries - QSC_ENTRY_TAIL, QSC_ENTRY_TAIL);
+                       d->s_entries - QSC_ENTRY_TAIL, QSC_ENTRY_TAIL, 0, d->K);
     hipLaunchKernelGGL(tail_fill_kernel<uint32_t>, tg, tb, 0, s, (uint32_t*)c_entries,
-                       d->c_entries - QSC_ENTRY_TAIL, QSC_ENTRY_TAIL);
+                       d->c_entries - QSC_ENTRY_TAIL, QSC_ENTRY_TAIL, 0, d->PT);
     hipLaunchKernelGGL(s_fill_kernel<uint32_t>, dim3((unsigned)ceil_div(d->Pp, kBlock)),
                        dim3(kBlock), 0, s, codes, perm, d->K, d->P, d->Pp, s_width, s_off,
-                       (uint32_t*)s_entries);
+                       (uint32_t*)s_entries, 0);
     QSC_CHECK_LAUNCH();
     hipLaunchKernelGGL(c_fill_kernel<uint32_t>, dim3((unsigned)d->ntiles), dim3(kBlock), 0, s,
                        codes, perm, d->K, d->P, d->PT, d->nks, c_width, c_off, c_kmap,
-                       (uint32_t*)c_entries);
+                       (uint32_t*)c_entries, 0);
   } else {
     hipLaunchKernelGGL(tail_fill_kernel<uint16_t>, tg, tb, 0, s, (uint16_t*)s_entries,
-                       d->s_entries - QSC_ENTRY_TAIL, QSC_ENTRY_TAIL);
+                       d->s_entries - QSC_ENTRY_TAIL, QSC_ENTRY_TAIL, sr, d->K);
     hipLaunchKernelGGL(tail_fill_kernel<uint16_t>, tg, tb, 0, s, (uint16_t*)c_entries,
-                       d->c_entries - QSC_ENTRY_TAIL, QSC_ENTRY_TAIL);
+                       d->c_entries - QSC_ENTRY_TAIL, QSC_ENTRY_TAIL, sr, d->PT);
     hipLaunchKernelGGL(s_fill_kernel<uint16_t>, dim3((unsigned)ceil_div(d->Pp, kBlock)),
                        dim3(kBlock), 0, s, codes, perm, d->K, d->P, d->Pp, s_width, s_off,
-                       (uint16_t*)s_entries);
+                       (uint16_t*)s_entries, sr);
     QSC_CHECK_LAUNCH();
     hipLaunchKernelGGL(c_fill_kernel<uint16_t>, dim3((unsigned)d->ntiles), dim3(kBlock), 0, s,
                        codes, perm, d->K, d->P, d->PT, d->nks, c_width, c_off, c_kmap,
-                       (uint16_t*)c_entries);
+                       (uint16_t*)c_entries, sr);
   }
   QSC_CHECK_LAUNCH();
   return QSC_OK;

@@ -82,6 +82,73 @@ template <int RP>
 struct Pitch {
   static constexpr int v = (RP == 4) ? 4 : RP + 4;
 };
+// Signed-row tables keep each row's signed threshold (the dot product's seed) either in the
+// row itself, floats RP, RP+1 = {thr~, +0} read as one 8-B LDS read (QSC_SR_THTAB 0), or in a
+// dense column of thr~/2 after the rows, one 4-B read (QSC_SR_THTAB 1: 64 banks apart, not 16)
+#ifndef QSC_SR_THTAB
+#define QSC_SR_THTAB 0
+#endif
+// table pitch of a likelihood kind
+template <int RP, int KIND>
+struct TP {
+  static constexpr int v = (KIND == LIK_ONEBIT_SR && !QSC_SR_THTAB) ? RP + 4 : Pitch<RP>::v;
+};
+constexpr bool is_sr(int kind) { return kind == LIK_ONEBIT_SR; }
+// rows of a table: K (C^T) or PT (S tile), or 2 * rows + 1 with signed rows
+template <int KIND>
+__device__ __host__ __forceinline__ int table_rows(int rows) {
+  return is_sr(KIND) ? 2 * rows + 1 : rows;
+}
+// floats of a gather table of `rows` rows (with its threshold column, if separate)
+template <int RP, int KIND>
+__device__ __host__ __forceinline__ int table_floats(int rows) {
+  return table_rows<KIND>(rows) * TP<RP, KIND>::v + ((is_sr(KIND) && QSC_SR_THTAB) ? table_rows<KIND>(rows) : 0);
+}
+template <int RP, int KIND>
+__device__ __host__ __forceinline__ int th_offset(int rows) {
+  return table_rows<KIND>(rows) * TP<RP, KIND>::v;
+}
+// the signed thresholds of rows i (+thr~) and rows + i (-thr~) of a signed-row table
+template <int RP, int KIND>
+__device__ __forceinline__ void put_th(float* tab, int rows, int i, float th) {
+  constexpr int P = TP<RP, KIND>::v;
+#if QSC_SR_THTAB
+  float* c = tab + th_offset<RP, KIND>(rows);
+  c[i] = 0.5f * th;
+  c[rows + i] = -0.5f * th;
+#else
+  *reinterpret_cast<float2*>(tab + i * P + RP) = make_float2(th, 0.0f);
+  *reinterpret_cast<float2*>(tab + (rows + i) * P + RP) = make_float2(-th, 0.0f);
+#endif
+}
+// row i of a gather table from 4-float groups v[0..RP): signed-row tables also get the threshold
+// in float RP and the negated copy at row rows + i
+template <int RP, int KIND>
+__device__ __forceinline__ void put_row4(float* tab, int rows, int i, int r, const float4& v,
+                                         float th) {
+  constexpr int P = TP<RP, KIND>::v;
+  *reinterpret_cast<float4*>(tab + i * P + r) = v;
+  if constexpr (is_sr(KIND)) {
+    *reinterpret_cast<float4*>(tab + (rows + i) * P + r) = make_float4(-v.x, -v.y, -v.z, -v.w);
+    if (r == 0) put_th<RP, KIND>(tab, rows, i, th);
+  }
+}
+// the neutral pad row 2 * rows of a signed-row table ([0, kPadZ]: P == 1, g == 0 exactly)
+template <int RP, int KIND>
+__device__ __forceinline__ void put_pad_row(float* tab, int rows) {
+  if constexpr (is_sr(KIND)) {
+    constexpr int P = TP<RP, KIND>::v;
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int r = 0; r < RP; ++r) tab[2 * rows * P + r] = 0.0f;
+#if QSC_SR_THTAB
+      tab[th_offset<RP, KIND>(rows) + 2 * rows] = 0.5f * kPadZ;
+#else
+      *reinterpret_cast<float2*>(tab + 2 * rows * P + RP) = make_float2(kPadZ, 0.0f);
+#endif
+    }
+  }
+}
 
 template <typename E>
 struct Ent;
@@ -167,12 +234,23 @@ __device__ __forceinline__ float dot2z(const f2v (&own)[RP / 2], const f2v (&o)[
   return r;
 }
 
+// the same with the seed pair read from a signed-row table ({thr~, +0}: no register move)
+template <int RP>
+__device__ __forceinline__ float dot2s(const f2v (&own)[RP / 2], const f2v (&o)[RP / 2], f2v seed) {
+  f2v d = fma2(own[0], o[0], seed);
+#pragma unroll
+  for (int j = 1; j < RP / 2; ++j) d = fma2(own[j], o[j], d);
+  float r = d.x + d.y;
+  asm("" : "+v"(r));
+  return r;
+}
+
 // factor the register row is pre-multiplied by: linear kinds evaluate in a scaled form
 // (lik_grad2): -1/a (general), -sqrt(log2 e)/a (one-bit); the log model / squared loss use t
 template <int KIND, bool LOG>
 __device__ __forceinline__ float own_scale_of(const Lik& lk) {
   if (LOG || KIND == LIK_SQUARED) return 1.0f;
-  return KIND == LIK_ONEBIT ? -lk.ob_scale : -lk.inv_a;
+  return (KIND == LIK_ONEBIT || KIND == LIK_ONEBIT_SR) ? -lk.ob_scale : -lk.inv_a;
 }
 
 struct Scalars {
@@ -186,21 +264,40 @@ struct Scalars {
 // moves them to z' = kPadZ where they contribute exactly 0, the other kinds mask them.  The NLL
 // is accumulated as a pair (summed by the caller).
 // the LDS rows of an entry pair (the gather half of pair_step)
-template <int RP, typename E>
+// (signed-row kind: the entry IS the row, whose float RP is the signed threshold -> tha/thb)
+template <int RP, typename E, int KIND>
 __device__ __forceinline__ void pair_rows(uint32_t ea, uint32_t eb, const f2v (&own)[RP / 2],
                                           const float* __restrict__ tab, f2v (&oa)[RP / 2],
-                                          f2v (&ob)[RP / 2]) {
+                                          f2v (&ob)[RP / 2], f2v& tha, f2v& thb, const Lik& lk) {
   using T = Ent<E>;
+  constexpr int P = TP<RP, KIND>::v;
+  const uint32_t ia = is_sr(KIND) ? ea : (ea & T::kMask), ib = is_sr(KIND) ? eb : (eb & T::kMask);
 #if QSC_DIAG_NOLDS  // diagnostic build: no gather (bounds the LDS share of the pass)
 #pragma unroll
   for (int j = 0; j < RP / 2; ++j) {
-    oa[j] = own[j] + splat2((float)(ea & T::kMask));
-    ob[j] = own[j] + splat2((float)(eb & T::kMask));
+    oa[j] = own[j] + splat2((float)ia);
+    ob[j] = own[j] + splat2((float)ib);
   }
+  tha = splat2((float)ia);
+  thb = splat2((float)ib);
 #else
   (void)own;
-  lds_row2<RP>(tab + (ea & T::kMask) * Pitch<RP>::v, oa);
-  lds_row2<RP>(tab + (eb & T::kMask) * Pitch<RP>::v, ob);
+  lds_row2<RP>(tab + ia * P, oa);
+  lds_row2<RP>(tab + ib * P, ob);
+  if constexpr (is_sr(KIND)) {
+#if QSC_DIAG_SR_NOTH  // diagnostic build: no threshold read (wrong values; bounds its LDS cost)
+    tha = thb = f2v{0.5f, 0.0f};
+#elif QSC_SR_THTAB
+    tha = splat2(tab[lk.th_off + ia]);  // {thr~/2, thr~/2}: the seed pair from one 4-B read
+    thb = splat2(tab[lk.th_off + ib]);
+#else
+    tha = *reinterpret_cast<const f2v*>(tab + ia * P + RP);
+    thb = *reinterpret_cast<const f2v*>(tab + ib * P + RP);
+#endif
+    (void)lk;
+  } else {
+    tha = thb = splat2(0.0f);
+  }
 #endif
 }
 
@@ -208,6 +305,7 @@ __device__ __forceinline__ void pair_rows(uint32_t ea, uint32_t eb, const f2v (&
 template <int RP, typename E, int KIND, bool LOG>
 __device__ __forceinline__ void pair_math(uint32_t ea, uint32_t eb, const f2v (&own)[RP / 2],
                                           const f2v (&oa)[RP / 2], const f2v (&ob)[RP / 2],
+                                          f2v tha, f2v thb,
                                           const float2* __restrict__ edges, const Lik& lk,
                                           f2v (&acc)[RP / 2], f2v& nll, bool valid);
 
@@ -217,17 +315,38 @@ __device__ __forceinline__ void pair_step(uint32_t ea, uint32_t eb, const f2v (&
                                           const float2* __restrict__ edges, const Lik& lk,
                                           f2v (&acc)[RP / 2], f2v& nll, bool valid) {
   f2v oa[RP / 2], ob[RP / 2];
-  pair_rows<RP, E>(ea, eb, own, tab, oa, ob);
-  pair_math<RP, E, KIND, LOG>(ea, eb, own, oa, ob, edges, lk, acc, nll, valid);
+  f2v tha, thb;
+  pair_rows<RP, E, KIND>(ea, eb, own, tab, oa, ob, tha, thb, lk);
+  pair_math<RP, E, KIND, LOG>(ea, eb, own, oa, ob, tha, thb, edges, lk, acc, nll, valid);
 }
 
 template <int RP, typename E, int KIND, bool LOG>
 __device__ __forceinline__ void pair_math(uint32_t ea, uint32_t eb, const f2v (&own)[RP / 2],
                                           const f2v (&oa)[RP / 2], const f2v (&ob)[RP / 2],
+                                          f2v tha, f2v thb,
                                           const float2* __restrict__ edges, const Lik& lk,
                                           f2v (&acc)[RP / 2], f2v& nll, bool valid) {
   using T = Ent<E>;
-  {
+  if constexpr (is_sr(KIND)) {
+    // signed rows: z~ = thr~ + own . row~ (both carry the entry's sign), no code / pad handling
+    f2v t = f2v{dot2s<RP>(own, oa, tha), dot2s<RP>(own, ob, thb)};
+    if (!valid) t = splat2(kPadZ);  // walk_masked's evaluations past a list end
+    f2v log2P, g;
+#if QSC_DIAG_NOMATH
+    g = t * splat2(1e-3f);
+    log2P = t;
+#else
+    lik_grad2<KIND, LOG>(t, 0, 0, false, false, edges, lk, log2P, g);
+#endif
+    nll -= log2P;
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j) acc[j] = fma2(splat2(g.x), oa[j], acc[j]);
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j) acc[j] = fma2(splat2(g.y), ob[j], acc[j]);
+    (void)ea;
+    (void)eb;
+    return;
+  } else {
     const int ca = (int)(ea >> T::kBits), cb = (int)(eb >> T::kBits);
     const bool pa = (ca == T::kPad) || !valid, pb = (cb == T::kPad) || !valid;
     f2v t;
@@ -318,10 +437,11 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
   // pair's arithmetic, so the LDS latency runs under it (the group's chunks are loaded, clamped,
   // so a prefetch past the list end reads valid rows that are never used)
   f2v ra[RP / 2], rb[RP / 2];
+  f2v tra, trb;
   {
     uint32_t e[4];
     Ent<E>::unpack(b[0], e);
-    pair_rows<RP, E>(e[0], e[1], own, tab, ra, rb);
+    pair_rows<RP, E, KIND>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
   }
 #endif
   for (;;) {
@@ -336,14 +456,15 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
         uint32_t e[4];
         Ent<E>::unpack(b[i], e);
         f2v xa[RP / 2], xb[RP / 2];
-        pair_rows<RP, E>(e[2], e[3], own, tab, xa, xb);
-        pair_math<RP, E, KIND, LOG>(e[0], e[1], own, ra, rb, edges, lk, acc, nll, true);
+        f2v txa, txb;
+        pair_rows<RP, E, KIND>(e[2], e[3], own, tab, xa, xb, txa, txb, lk);
+        pair_math<RP, E, KIND, LOG>(e[0], e[1], own, ra, rb, tra, trb, edges, lk, acc, nll, true);
         if (i + 1 < kGroup) {
           uint32_t f[4];
           Ent<E>::unpack(b[i + 1], f);
-          pair_rows<RP, E>(f[0], f[1], own, tab, ra, rb);
+          pair_rows<RP, E, KIND>(f[0], f[1], own, tab, ra, rb, tra, trb, lk);
         }
-        pair_math<RP, E, KIND, LOG>(e[2], e[3], own, xa, xb, edges, lk, acc, nll, true);
+        pair_math<RP, E, KIND, LOG>(e[2], e[3], own, xa, xb, txa, txb, edges, lk, acc, nll, true);
       }
     if (!more) break;
 #pragma unroll
@@ -351,7 +472,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
     {
       uint32_t e[4];
       Ent<E>::unpack(b[0], e);
-      pair_rows<RP, E>(e[0], e[1], own, tab, ra, rb);
+      pair_rows<RP, E, KIND>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
     }
 #else
 #pragma unroll
@@ -661,15 +782,17 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     float* __restrict__ vS, qsc_adam ad, float lambda_s, qsc_state* __restrict__ st,
     float* __restrict__ part_nll, float* __restrict__ part_nsq, int* __restrict__ sched,
     AdamCache* __restrict__ acache) {
-  constexpr int CP = Pitch<RP>::v;
+  constexpr int CP = TP<RP, KIND>::v;
   constexpr int RH = RP / 2;  // row elements updated per lane (half row)
   // linear models evaluate the entries in a scaled form (lik_grad2)
   const float own_scale = own_scale_of<KIND, LOG>(lk);
   // all LDS carved from the 16-B aligned dynamic region (no statics ahead of it)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   Scalars& sc = *reinterpret_cast<Scalars*>(smem);            // 32 B reserved
-  float* Cl = smem + 8;                                        // [K][CP]
-  float2* El = reinterpret_cast<float2*>(Cl + (size_t)K * CP);  // [nbins]
+  float* Cl = smem + 8;                                        // [K][CP] (signed rows: [2K+1])
+  float2* El = reinterpret_cast<float2*>(Cl + (size_t)table_floats<RP, KIND>(K));  // [nbins]
+  Lik lks = lk;  // the C^T table's threshold column
+  lks.th_off = th_offset<RP, KIND>(K);
 
   // a wave = one slice of QSC_SLICE (32) pixel positions at a time, two lanes per pixel: lane
   // half h takes entries 2h, 2h+1 of every 4-entry chunk of the pixel's list; the halves'
@@ -712,9 +835,10 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     const int kw = min(k0, K - 1);
 #pragma unroll
     for (int r = 0; r < RP; r += 4)
-      *reinterpret_cast<float4*>(Cl + kw * CP + r) =
-          make_float4(r < R ? c0[r] : 0.0f, r + 1 < R ? c0[r + 1] : 0.0f,
-                      r + 2 < R ? c0[r + 2] : 0.0f, r + 3 < R ? c0[r + 3] : 0.0f);
+      put_row4<RP, KIND>(Cl, K, kw, r,
+                         make_float4(r < R ? c0[r] : 0.0f, r + 1 < R ? c0[r + 1] : 0.0f,
+                                     r + 2 < R ? c0[r + 2] : 0.0f, r + 3 < R ? c0[r + 3] : 0.0f),
+                         lk.ob_thr);
   }
   for (int k = k0 + kSBlock; k < K; k += kSBlock) {
     float v[RP];
@@ -722,8 +846,9 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     for (int r = 0; r < RP; ++r) v[r] = (r < R) ? C[(int64_t)r * K + k] : 0.0f;
 #pragma unroll
     for (int r = 0; r < RP; r += 4)
-      *reinterpret_cast<float4*>(Cl + k * CP + r) = make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
+      put_row4<RP, KIND>(Cl, K, k, r, make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]), lk.ob_thr);
   }
+  put_pad_row<RP, KIND>(Cl, K);
   El[min(k0, nbins - 1)] = e0;  // branch-free like C^T
   for (int b = k0 + kSBlock; b < nbins; b += kSBlock) El[b] = E_.e[b];
   if (threadIdx.x == 0) {
@@ -769,7 +894,7 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_halves<RP, E, KIND, LOG>(c.src, ln.ent, 2 * QSC_SLICE, c.j1, c.buf, own, Cl, El, lk,
+    walk_halves<RP, E, KIND, LOG>(c.src, ln.ent, 2 * QSC_SLICE, c.j1, c.buf, own, Cl, El, lks,
                                   accp, nll);
     STAMP(w, 3 + 3 * i);
     // the two lane halves' partial dS: v_permlane32_swap (VALU) instead of an LDS shuffle
@@ -846,11 +971,15 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
     float* __restrict__ part_nll, float* __restrict__ cnsq) {
   using T = Ent<E>;
   using V4 = typename T::V4;
-  constexpr int SP = Pitch<RP>::v;
+  constexpr int SP = TP<RP, KIND>::v;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* Sl = smem;                                              // [PT][SP]
-  float2* El = reinterpret_cast<float2*>(Sl + (size_t)PT * SP);   // [nbins] (<= 254)
-  float* Pl = Sl + (size_t)PT * SP + 2 * 256;                     // [kCParts][R][64]
+  const int TR = table_rows<KIND>(PT);
+  float* Sl = smem;                                              // [PT][SP] (signed: [2PT+1])
+  float2* El = reinterpret_cast<float2*>(Sl + (size_t)table_floats<RP, KIND>(PT));  // [nbins]
+  float* Pl = Sl + (size_t)table_floats<RP, KIND>(PT) + 2 * 256;  // [kCParts][R][64]
+  (void)TR;
+  Lik lkc = lk;  // the S tile's threshold column
+  lkc.th_off = th_offset<RP, KIND>(PT);
   float* Nl = Pl + (size_t)kCParts * R * 64;                      // [kCParts]
   int t, ks;
   if (xcd_map) {
@@ -890,8 +1019,9 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
 #pragma unroll 4
     for (int i = threadIdx.x; i < PT * V; i += kCBlock) {
       const int ql = i / V, c = i - ql * V;
-      *reinterpret_cast<float4*>(Sl + ql * SP + 4 * c) = src4[tile_pos(t, ql, nt) * V + c];
+      put_row4<RP, KIND>(Sl, PT, ql, 4 * c, src4[tile_pos(t, ql, nt) * V + c], lk.ob_thr);
     }
+    put_pad_row<RP, KIND>(Sl, PT);
   }
   for (int i = threadIdx.x; i < nbins; i += kCBlock) El[i] = E_.e[i];
   __syncthreads();
@@ -909,9 +1039,9 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
   f2v nll = splat2(0.0f);
 #if QSC_CPASS_MASKED
-  walk_masked<RP, E, KIND, LOG>(src, lo, 64, j0, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+  walk_masked<RP, E, KIND, LOG>(src, lo, 64, j0, j0, j1, 1, buf, own, Sl, El, lkc, accp, nll);
 #else
-  walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+  walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lkc, accp, nll);
 #endif
   STAMP(wg, 2);
   const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
@@ -967,13 +1097,17 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
     float* __restrict__ part_nll, float* __restrict__ cnsq) {
   using T = Ent<E>;
   using V4 = typename T::V4;
-  constexpr int SP = Pitch<RP>::v;
+  constexpr int SP = TP<RP, KIND>::v;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int NW = blockDim.x >> 6;
   const int U = nks * NP;
-  float* Sl = smem;                                              // [PT][SP]
-  float2* El = reinterpret_cast<float2*>(Sl + (size_t)PT * SP);   // [nbins] (<= 254)
-  float* Pl = Sl + (size_t)PT * SP + 2 * 256;                     // [U][R][64]   (NP > 1)
+  const int TR = table_rows<KIND>(PT);
+  float* Sl = smem;                                              // [PT][SP] (signed: [2PT+1])
+  float2* El = reinterpret_cast<float2*>(Sl + (size_t)table_floats<RP, KIND>(PT));  // [nbins]
+  float* Pl = Sl + (size_t)table_floats<RP, KIND>(PT) + 2 * 256;  // [U][R][64]   (NP > 1)
+  (void)TR;
+  Lik lkc = lk;  // the S tile's threshold column
+  lkc.th_off = th_offset<RP, KIND>(PT);
   float* Nl = Pl + (NP > 1 ? (size_t)U * R * 64 : 0);             // [U] / [NW]
   const int t = blockIdx.x;
   const int Kp = nks * 64;
@@ -1012,8 +1146,9 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
 #pragma unroll 4
     for (int i = threadIdx.x; i < PT * V; i += blockDim.x) {
       const int ql = i / V, c = i - ql * V;
-      *reinterpret_cast<float4*>(Sl + ql * SP + 4 * c) = src4[tile_pos(t, ql, nt) * V + c];
+      put_row4<RP, KIND>(Sl, PT, ql, 4 * c, src4[tile_pos(t, ql, nt) * V + c], lk.ob_thr);
     }
+    put_pad_row<RP, KIND>(Sl, PT);
   }
   for (int i = threadIdx.x; i < nbins; i += blockDim.x) El[i] = E_.e[i];
   __syncthreads();
@@ -1030,7 +1165,7 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lkc, accp, nll);
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (NP == 1) {
       // the unit is the whole (tile, k-slice): its slab rows straight from registers
@@ -1081,11 +1216,21 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
 }
 
 // LDS bytes of cpass_tile_kernel
-size_t cpass_tile_lds(int PT, int R, int nks, int NP) {
+// pitch (floats) and row count of a gather table (sr: signed rows)
+inline int tpitch(int R, bool sr) {
   const int RP = R <= 4 ? 4 : (R <= 8 ? 8 : 16);
+  return ((sr && !QSC_SR_THTAB) || RP > 4) ? RP + 4 : 4;
+}
+inline size_t trows(int rows, bool sr) { return sr ? 2 * (size_t)rows + 1 : (size_t)rows; }
+// floats of a gather table (rows at the pitch, plus a separate threshold column if any)
+inline size_t tfloats(int rows, int R, bool sr) {
+  return trows(rows, sr) * tpitch(R, sr) + ((sr && QSC_SR_THTAB) ? trows(rows, sr) : 0);
+}
+
+size_t cpass_tile_lds(int PT, int R, int nks, int NP, bool sr) {
   const size_t U = (size_t)nks * NP;
-  return (size_t)PT * (RP == 4 ? 4 : RP + 4) * 4 + 2 * 256 * 4 +
-         (NP > 1 ? U * R * 64 * 4 : 0) + std::max<size_t>(U, 16) * 4;
+  return tfloats(PT, R, sr) * 4 + 2 * 256 * 4 + (NP > 1 ? U * R * 64 * 4 : 0) +
+         std::max<size_t>(U, 16) * 4;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1118,15 +1263,18 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
     float* __restrict__ part_nsq_s, float* __restrict__ slab, float* __restrict__ part_nll_c,
     float* __restrict__ cnsq, AdamCache* __restrict__ acache) {
   using V4 = typename Ent<E>::V4;
-  constexpr int CP = Pitch<RP>::v;  // C^T row pitch == S tile row pitch
+  constexpr int CP = TP<RP, KIND>::v;  // C^T row pitch == S tile row pitch
   constexpr int RH = RP / 2;
   constexpr bool ADAM = true;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   Scalars& sc = *reinterpret_cast<Scalars*>(smem);                // 32 B
-  float* Cl = smem + 8;                                            // [K][CP]
-  float2* El = reinterpret_cast<float2*>(Cl + (size_t)K * CP);      // [256]
-  float* Sl = reinterpret_cast<float*>(El + 256);                   // [PT][CP]
-  float* Pl = Sl + (size_t)PT * CP;                                 // [U][R][64]  (NP > 1)
+  float* Cl = smem + 8;                                            // [K][CP] (signed: 2K+1)
+  float2* El = reinterpret_cast<float2*>(Cl + (size_t)table_floats<RP, KIND>(K));  // [256]
+  float* Sl = reinterpret_cast<float*>(El + 256);                   // [PT][CP] (signed: 2PT+1)
+  float* Pl = Sl + (size_t)table_floats<RP, KIND>(PT);              // [U][R][64]  (NP > 1)
+  Lik lks = lk, lkc = lk;  // the threshold columns of C^T (S-step) and of the S tile (C-pass)
+  lks.th_off = th_offset<RP, KIND>(K);
+  lkc.th_off = th_offset<RP, KIND>(PT);
   const int NW = blockDim.x >> 6;
   const int U = nks * NP;
   float* Nl = Pl + (NP > 1 ? (size_t)U * R * 64 : 0);               // [max(U,16)]
@@ -1209,6 +1357,12 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
         Cl[(k + 1) * CP + r] = v.y;
         Cl[(k + 2) * CP + r] = v.z;
         Cl[(k + 3) * CP + r] = v.w;
+        if constexpr (is_sr(KIND)) {
+          Cl[(K + k) * CP + r] = -v.x;
+          Cl[(K + k + 1) * CP + r] = -v.y;
+          Cl[(K + k + 2) * CP + r] = -v.z;
+          Cl[(K + k + 3) * CP + r] = -v.w;
+        }
       };
       if (k0 < n4) put(k0, cq);
       for (int i = k0 + (int)blockDim.x; i < n4; i += blockDim.x)
@@ -1216,25 +1370,35 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
       for (int i = k0; i < K * (RP - R); i += blockDim.x) {  // rows R..RP-1 are zero
         const int k = i / (RP - R), r = R + (i - k * (RP - R));
         Cl[k * CP + r] = 0.0f;
+        if constexpr (is_sr(KIND)) Cl[(K + k) * CP + r] = -0.0f;
       }
+      if constexpr (is_sr(KIND))
+        for (int k = k0; k < K; k += blockDim.x) put_th<RP, KIND>(Cl, K, k, lk.ob_thr);
     } else
 #endif
     {
       const int kw = min(k0, K - 1);  // branch-free: threads past K rewrite row K-1
 #pragma unroll
       for (int r = 0; r < RP; r += 4)
-        *reinterpret_cast<float4*>(Cl + kw * CP + r) =
-            make_float4(r < R ? c0[r] : 0.0f, r + 1 < R ? c0[r + 1] : 0.0f,
-                        r + 2 < R ? c0[r + 2] : 0.0f, r + 3 < R ? c0[r + 3] : 0.0f);
+        put_row4<RP, KIND>(Cl, K, kw, r,
+                           make_float4(r < R ? c0[r] : 0.0f, r + 1 < R ? c0[r + 1] : 0.0f,
+                                       r + 2 < R ? c0[r + 2] : 0.0f, r + 3 < R ? c0[r + 3] : 0.0f),
+                           lk.ob_thr);
       for (int k = k0 + (int)blockDim.x; k < K; k += blockDim.x) {
         float v[RP];
 #pragma unroll
         for (int r = 0; r < RP; ++r) v[r] = (r < R) ? C[(int64_t)r * K + k] : 0.0f;
 #pragma unroll
         for (int r = 0; r < RP; r += 4)
-          *reinterpret_cast<float4*>(Cl + k * CP + r) =
-              make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
+          put_row4<RP, KIND>(Cl, K, k, r, make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]),
+                             lk.ob_thr);
       }
+    }
+    put_pad_row<RP, KIND>(Cl, K);
+    if constexpr (is_sr(KIND)) {
+      // the S tile's threshold column and pad row (its S values are written by the S-step)
+      for (int q = k0; q < PT; q += blockDim.x) put_th<RP, KIND>(Sl, PT, q, lk.ob_thr);
+      put_pad_row<RP, KIND>(Sl, PT);
     }
     El[min(k0, nbins - 1)] = e0;
     for (int b = k0 + (int)blockDim.x; b < nbins; b += blockDim.x) El[b] = E_.e[b];
@@ -1305,7 +1469,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_halves<RP, E, KIND, LOG>(c.src, ln.ent, 2 * QSC_SLICE, c.j1, c.buf, own, Cl, El, lk,
+    walk_halves<RP, E, KIND, LOG>(c.src, ln.ent, 2 * QSC_SLICE, c.j1, c.buf, own, Cl, El, lks,
                                   accp, nll);
     float acc[RP];
 #pragma unroll
@@ -1327,6 +1491,12 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
     st_row<RH>(mS + blk, ln.half, m);
     st_row<RH>(vS + blk, ln.half, v);
     st_row<RH>(Sl + (il * QSC_SLICE + p) * CP + h * RH, pv);  // the tile row, for the C-pass
+    if constexpr (is_sr(KIND)) {
+      float nv[RH];
+#pragma unroll
+      for (int j = 0; j < RH; ++j) nv[j] = -pv[j];
+      st_row<RH>(Sl + (PT + il * QSC_SLICE + p) * CP + h * RH, nv);
+    }
     nsq = wave_sum_dpp(nsq);
     if (lane == 0) part_nsq_s[s] = nsq;
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
@@ -1381,7 +1551,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lkc, accp, nll);
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (NP == 1) {
 #pragma unroll
@@ -1427,11 +1597,9 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
 }
 
 // LDS bytes of scfused_kernel
-size_t scfused_lds(int PT, int R, int K, int nks, int NP) {
-  const int RP = R <= 4 ? 4 : (R <= 8 ? 8 : 16);
-  const int CP = RP == 4 ? 4 : RP + 4;
+size_t scfused_lds(int PT, int R, int K, int nks, int NP, bool sr) {
   const size_t U = (size_t)nks * NP;
-  return 32 + (size_t)K * CP * 4 + 256 * 8 + (size_t)PT * CP * 4 +
+  return 32 + tfloats(K, R, sr) * 4 + 256 * 8 + tfloats(PT, R, sr) * 4 +
          (NP > 1 ? U * R * 64 * 4 : 0) + std::max<size_t>(U, 16) * 4;
 }
 
@@ -1809,11 +1977,13 @@ int cu_count() {
 #define QSC_SPASS_BPC 2
 #endif
 
-size_t cpass_lds(const qsc_obs_desc* d, int R) {
-  const int RP = rp_of(R);
-  return (size_t)d->PT * (RP == 4 ? 4 : RP + 4) * 4 + 2 * 256 * 4 + (size_t)kCParts * R * 64 * 4 +
-         kCParts * 4;
+size_t cpass_lds(const qsc_obs_desc* d, int R, bool sr) {
+  return tfloats(d->PT, R, sr) * 4 + 2 * 256 * 4 + (size_t)kCParts * R * 64 * 4 + kCParts * 4;
 }
+size_t spass_lds(const qsc_obs_desc* d, int R, bool sr) {
+  return 32 + tfloats(d->K, R, sr) * 4 + (size_t)d->nbins * 8;
+}
+int spass_bpc(int RP) { return RP > 8 ? 2 : RP == 8 ? QSC_SPASS_BPC8 : QSC_SPASS_BPC; }
 
 }  // namespace
 
@@ -1832,14 +2002,24 @@ size_t cpass_lds(const qsc_obs_desc* d, int R) {
       else LAUNCH(16, uint16_t, KD, LG);                                                 \
     }                                                                                    \
   } while (0)
+// signed-row layouts (rowfmt 1) are narrow and one-bit only
+#define QSC_DISPATCH_RP_NARROW(LAUNCH, KD, LG)                                           \
+  do {                                                                                   \
+    if (RP == 4) LAUNCH(4, uint16_t, KD, LG);                                            \
+    else if (RP == 8) LAUNCH(8, uint16_t, KD, LG);                                       \
+    else LAUNCH(16, uint16_t, KD, LG);                                                   \
+  } while (0)
 #define QSC_DISPATCH_PASS(LAUNCH)                                                        \
   do {                                                                                   \
-    if (kind == LIK_ONEBIT) QSC_DISPATCH_RP(LAUNCH, LIK_ONEBIT, false);                  \
+    if (sr) QSC_DISPATCH_RP_NARROW(LAUNCH, LIK_ONEBIT_SR, false);                        \
+    else if (kind == LIK_ONEBIT) QSC_DISPATCH_RP(LAUNCH, LIK_ONEBIT, false);             \
     else if (kind == LIK_SQUARED && m->log_model) QSC_DISPATCH_RP(LAUNCH, LIK_SQUARED, true); \
     else if (kind == LIK_SQUARED) QSC_DISPATCH_RP(LAUNCH, LIK_SQUARED, false);           \
     else if (m->log_model) QSC_DISPATCH_RP(LAUNCH, LIK_GENERAL, true);                   \
     else QSC_DISPATCH_RP(LAUNCH, LIK_GENERAL, false);                                    \
   } while (0)
+
+static bool rowfmt_ok(const qsc_obs_desc* d, int R, int kind);
 
 extern "C" {
 
@@ -1879,19 +2059,21 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
   if (mode == 1 && (!mS || !vS || !adam)) return QSC_EINVAL;
   if (mode != 0 && mode != 1) return QSC_EINVAL;
   const int RP = rp_of(R);
-  const size_t shm = 32 + (size_t)d->K * (RP == 4 ? 4 : RP + 4) * 4 + (size_t)d->nbins * 8;
+  const int kind = lik_kind(m);
+  const bool sr = d->rowfmt == 1;
+  if (!rowfmt_ok(d, R, kind)) return QSC_EINVAL;
+  const size_t shm = spass_lds(d, R, sr);
   if (shm > 160 * 1024) return QSC_EINVAL;
   PassWs w = carve(d, R, ws);
   Edges E;
   make_edges(m, &E);
   const Lik lk = make_lik(m);
-  const int kind = lik_kind(m);
   if (kind == LIK_SQUARED)
     make_sq_targets(m, &E);
   else if (!m->log_model)
     scale_edges(&E, m->nbounds - 1, lk.a);
   const int nslices = d->Pp / QSC_SLICE;
-  const int bpc = RP > 8 ? 2 : RP == 8 ? QSC_SPASS_BPC8 : QSC_SPASS_BPC;
+  const int bpc = spass_bpc(RP);
   const dim3 grid((unsigned)std::min<int64_t>(ceil_div(nslices, kSWaves), (int64_t)cu_count() * bpc));
   qsc_adam ad{};
   if (adam) ad = *adam;
@@ -1923,13 +2105,14 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
       ws_bytes < ws_bytes_for(d, R))
     return QSC_EINVAL;
   const int RP = rp_of(R);
-  const size_t shm = cpass_lds(d, R);
-  if (shm > 160 * 1024) return QSC_EINVAL;
+  const int kind = lik_kind(m);
+  const bool sr = d->rowfmt == 1;
+  if (!rowfmt_ok(d, R, kind)) return QSC_EINVAL;
+  const size_t shm = cpass_lds(d, R, sr);
   PassWs w = carve(d, R, ws);
   Edges E;
   make_edges(m, &E);
   const Lik lk = make_lik(m);
-  const int kind = lik_kind(m);
   if (kind == LIK_SQUARED)
     make_sq_targets(m, &E);
   else if (!m->log_model)
@@ -1948,7 +2131,7 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
     const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
     while (NP > 1 && chunks / NP < 3.0) --NP;
     const int U = nks * NP;
-    const size_t tshm = cpass_tile_lds(d->PT, R, nks, NP);
+    const size_t tshm = cpass_tile_lds(d->PT, R, nks, NP, sr);
     if (U >= 4 && tshm <= 160 * 1024) {
       const dim3 tb((unsigned)(64 * std::min(U, QSC_CTILE_MAXW)));
 #define CPASS_TILE_LAUNCH(RPV, ET, KD, LG)                                                     \
@@ -1961,6 +2144,7 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
       return QSC_OK;
     }
   }
+  if (shm > 160 * 1024) return QSC_EINVAL;
   const int xcd_map = (d->ntiles % 8) == 0 ? 1 : 0;
   const dim3 grid((unsigned)((int64_t)d->ntiles * d->nks));
 #define CPASS_LAUNCH(RPV, ET, KD, LG)                                                          \
@@ -1982,14 +2166,50 @@ static int cpass_parts(const qsc_obs_desc* d) {
   return NP;
 }
 
-QSC_API int qsc_scpass_supported(const qsc_obs_desc* d, int32_t R) {
-  if (!desc_ok(d) || R < 1 || R > 16) return 0;
+// the fused launch applies (its C-pass partition and LDS fit), with or without signed rows
+static bool scpass_fits(const qsc_obs_desc* d, int R, bool sr) {
   const int NP = cpass_parts(d);
   const int U = d->nks * NP;
-  return (U >= 4 && U <= QSC_CTILE_MAXW && d->PT <= 4096 &&
-          scfused_lds(d->PT, R, d->K, d->nks, NP) <= 160 * 1024)
-             ? 1
-             : 0;
+  return U >= 4 && U <= QSC_CTILE_MAXW && d->PT <= 4096 &&
+         scfused_lds(d->PT, R, d->K, d->nks, NP, sr) <= 160 * 1024;
+}
+
+// Signed-row layouts (include/qsc.h rowfmt 1): the one-bit kind, narrow entries whose values
+// reach row 2K / 2PT, and every pass form the code-field layout would use still fitting its
+// LDS (the S-pass at its resident-block count; the C-pass tile form or, where that does not
+// apply, the per-slice form; the fused launch where it applies)
+static bool sr_layout_ok(const qsc_obs_desc* d, int R) {
+  if (d->wide || d->nbins != 2 || 2 * (int64_t)d->K > 0xFFFF || 2 * (int64_t)d->PT > 0xFFFF)
+    return false;
+  const int RP = rp_of(R);
+  if (spass_lds(d, R, true) * spass_bpc(RP) > 160 * 1024) return false;
+  const int nks = d->nks;
+  int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
+  const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
+  while (NP > 1 && chunks / NP < 3.0) --NP;
+  const bool tile = QSC_CPASS_TILE && nks * NP >= 4 &&
+                    cpass_tile_lds(d->PT, R, nks, NP, false) <= 160 * 1024;
+  if (tile ? cpass_tile_lds(d->PT, R, nks, NP, true) > 160 * 1024
+           : cpass_lds(d, R, true) > 160 * 1024)
+    return false;
+  if (scpass_fits(d, R, false) && !scpass_fits(d, R, true)) return false;
+  return true;
+}
+
+// a launch's layout / likelihood-kind pairing: signed rows need the one-bit kind
+static bool rowfmt_ok(const qsc_obs_desc* d, int R, int kind) {
+  if (d->rowfmt == 0) return true;
+  return d->rowfmt == 1 && kind == LIK_ONEBIT && sr_layout_ok(d, R);
+}
+
+QSC_API int qsc_obs_signed_rows_ok(const qsc_obs_desc* d, int32_t R, const qsc_model* m) {
+  if (!desc_ok(d) || !m || R < 1 || R > QSC_MAX_R || m->nbounds - 1 != d->nbins) return 0;
+  return (lik_kind(m) == LIK_ONEBIT && sr_layout_ok(d, R)) ? 1 : 0;
+}
+
+QSC_API int qsc_scpass_supported(const qsc_obs_desc* d, int32_t R) {
+  if (!desc_ok(d) || R < 1 || R > 16) return 0;
+  return scpass_fits(d, R, d->rowfmt == 1) ? 1 : 0;
 }
 
 QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
@@ -2004,12 +2224,14 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
     return QSC_EINVAL;
   const int RP = rp_of(R);
   const int NP = cpass_parts(d);
-  const size_t shm = scfused_lds(d->PT, R, d->K, d->nks, NP);
+  const int kind = lik_kind(m);
+  const bool sr = d->rowfmt == 1;
+  if (!rowfmt_ok(d, R, kind)) return QSC_EINVAL;
+  const size_t shm = scfused_lds(d->PT, R, d->K, d->nks, NP, sr);
   PassWs w = carve(d, R, ws);
   Edges E;
   make_edges(m, &E);
   const Lik lk = make_lik(m);
-  const int kind = lik_kind(m);
   if (kind == LIK_SQUARED)
     make_sq_targets(m, &E);
   else if (!m->log_model)

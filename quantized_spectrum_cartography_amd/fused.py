@@ -25,6 +25,7 @@ class PassEngine:
         if not 1 <= R <= _lib.QSC_MAX_R:
             raise ValueError("rank R must be in [1, %d]" % _lib.QSC_MAX_R)
         self.obs, self.R = obs, R
+        obs.ensure_rank(R)
         dev = obs.device
         nb = _lib.lib().qsc_pass_workspace_bytes(obs.desc, R)
         if nb == 0:

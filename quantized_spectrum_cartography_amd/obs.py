@@ -118,9 +118,27 @@ class Observations:
         et = torch.int32 if desc.wide else torch.int16
         self.s_entries = torch.empty(desc.s_entries, dtype=et, device=dev)
         self.c_entries = torch.empty(desc.c_entries, dtype=et, device=dev)
-        _lib.call("qsc_obs_fill", _lib.ptr(codes), desc, _lib.ptr(perm), _lib.ptr(self.s_width),
-                  _lib.ptr(self.s_off), _lib.ptr(self.c_width), _lib.ptr(self.c_off),
-                  _lib.ptr(self.c_kmap), _lib.ptr(self.s_entries), _lib.ptr(self.c_entries), s)
+        # signed-row entries (include/qsc.h rowfmt 1: the one-bit kind reads each entry's code
+        # through the gathered row) wherever the passes' doubled tables fit at this rank
+        self._fill(1 if self.signed_rows_ok(R_hint) else 0)
+
+    def _fill(self, rowfmt):
+        self.desc.rowfmt = int(rowfmt)
+        _lib.call("qsc_obs_fill", _lib.ptr(self.codes), self.desc, _lib.ptr(self.perm),
+                  _lib.ptr(self.s_width), _lib.ptr(self.s_off), _lib.ptr(self.c_width),
+                  _lib.ptr(self.c_off), _lib.ptr(self.c_kmap), _lib.ptr(self.s_entries),
+                  _lib.ptr(self.c_entries), _lib.stream())
+
+    def signed_rows_ok(self, R):
+        if os.environ.get("QSC_SIGNED_ROWS", "1") == "0":  # A/B switch (tuning runs)
+            return False
+        return bool(_lib.lib().qsc_obs_signed_rows_ok(self.desc, int(R), self.model))
+
+    def ensure_rank(self, R):
+        """Re-pack in the code-field format if the signed-row layout chosen for R_hint does not
+        apply at rank R (the entry count is the same; only the values change)."""
+        if self.desc.rowfmt == 1 and not self.signed_rows_ok(R):
+            self._fill(0)
 
     # ---- info -----------------------------------------------------------------------
     @property
@@ -135,6 +153,7 @@ class Observations:
         d = self.desc
         return dict(K=d.K, P=d.P, Pp=d.Pp, tile=d.PT, ntiles=d.ntiles, nks=d.nks, wide=d.wide,
                     nbins=d.nbins, nnz=d.nnz, s_entries=d.s_entries, c_entries=d.c_entries,
+                    rowfmt=d.rowfmt,
                     s_padding=d.s_entries / max(d.nnz, 1) - 1.0,
                     c_padding=d.c_entries / max(d.nnz, 1) - 1.0)
 
