@@ -193,7 +193,6 @@ struct Lik {
   float ob_scale; // fp32(sqrt(log2 e) / a): the factor rows are pre-scaled by -ob_scale
   float ob_thr;   // fp32(thr * sqrt(log2 e) / a)
   float ob_kg;    // fp32(kgrad / kMillsK)
-  int th_off;     // signed-row kind: float offset of the gather table's threshold column
 };
 
 // one-bit Mills-ratio form.  With c = sqrt(log2 e) and u = c |z|, the probit tail
@@ -229,7 +228,6 @@ inline Lik make_lik(const qsc_model* m) {
   l.ob_scale = (float)(c / (double)l.a);
   l.ob_thr = (float)((double)l.thr * c / (double)l.a);
   l.ob_kg = (float)((double)p.kgrad / kMillsK);
-  l.th_off = 0;
 #if QSC_FTZ_SAT
   l.ob_kg = (float)((double)p.kgrad / kMillsK * 0x1p101);  // E is carried 2^-101 low
 #endif

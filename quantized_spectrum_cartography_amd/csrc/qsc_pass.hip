@@ -82,16 +82,14 @@ template <int RP>
 struct Pitch {
   static constexpr int v = (RP == 4) ? 4 : RP + 4;
 };
-// Signed-row tables keep each row's signed threshold (the dot product's seed) either in the
-// row itself, floats RP, RP+1 = {thr~, +0} read as one 8-B LDS read (QSC_SR_THTAB 0), or in a
-// dense column of thr~/2 after the rows, one 4-B read (QSC_SR_THTAB 1: 64 banks apart, not 16)
-#ifndef QSC_SR_THTAB
-#define QSC_SR_THTAB 0
-#endif
+// Signed-row tables keep each row's signed threshold (the dot product's seed) in the row
+// itself: floats RP, RP+1 = {thr~, +0}, one 8-B LDS read per entry.  (A dense column of thr~/2
+// after the rows, one 4-B read with the rows' banks spread 64 ways instead of 16, measured
+// slower: 31.75 vs 30.97 us for the fused launch, the extra address VALU outweighing it.)
 // table pitch of a likelihood kind
 template <int RP, int KIND>
 struct TP {
-  static constexpr int v = (KIND == LIK_ONEBIT_SR && !QSC_SR_THTAB) ? RP + 4 : Pitch<RP>::v;
+  static constexpr int v = KIND == LIK_ONEBIT_SR ? RP + 4 : Pitch<RP>::v;
 };
 constexpr bool is_sr(int kind) { return kind == LIK_ONEBIT_SR; }
 // rows of a table: K (C^T) or PT (S tile), or 2 * rows + 1 with signed rows
@@ -99,27 +97,17 @@ template <int KIND>
 __device__ __host__ __forceinline__ int table_rows(int rows) {
   return is_sr(KIND) ? 2 * rows + 1 : rows;
 }
-// floats of a gather table of `rows` rows (with its threshold column, if separate)
+// floats of a gather table of `rows` rows
 template <int RP, int KIND>
 __device__ __host__ __forceinline__ int table_floats(int rows) {
-  return table_rows<KIND>(rows) * TP<RP, KIND>::v + ((is_sr(KIND) && QSC_SR_THTAB) ? table_rows<KIND>(rows) : 0);
-}
-template <int RP, int KIND>
-__device__ __host__ __forceinline__ int th_offset(int rows) {
   return table_rows<KIND>(rows) * TP<RP, KIND>::v;
 }
 // the signed thresholds of rows i (+thr~) and rows + i (-thr~) of a signed-row table
 template <int RP, int KIND>
 __device__ __forceinline__ void put_th(float* tab, int rows, int i, float th) {
   constexpr int P = TP<RP, KIND>::v;
-#if QSC_SR_THTAB
-  float* c = tab + th_offset<RP, KIND>(rows);
-  c[i] = 0.5f * th;
-  c[rows + i] = -0.5f * th;
-#else
   *reinterpret_cast<float2*>(tab + i * P + RP) = make_float2(th, 0.0f);
   *reinterpret_cast<float2*>(tab + (rows + i) * P + RP) = make_float2(-th, 0.0f);
-#endif
 }
 // row i of a gather table from 4-float groups v[0..RP): signed-row tables also get the threshold
 // in float RP and the negated copy at row rows + i
@@ -141,11 +129,7 @@ __device__ __forceinline__ void put_pad_row(float* tab, int rows) {
     if (threadIdx.x == 0) {
 #pragma unroll
       for (int r = 0; r < RP; ++r) tab[2 * rows * P + r] = 0.0f;
-#if QSC_SR_THTAB
-      tab[th_offset<RP, KIND>(rows) + 2 * rows] = 0.5f * kPadZ;
-#else
       *reinterpret_cast<float2*>(tab + 2 * rows * P + RP) = make_float2(kPadZ, 0.0f);
-#endif
     }
   }
 }
@@ -287,14 +271,11 @@ __device__ __forceinline__ void pair_rows(uint32_t ea, uint32_t eb, const f2v (&
   if constexpr (is_sr(KIND)) {
 #if QSC_DIAG_SR_NOTH  // diagnostic build: no threshold read (wrong values; bounds its LDS cost)
     tha = thb = f2v{0.5f, 0.0f};
-#elif QSC_SR_THTAB
-    tha = splat2(tab[lk.th_off + ia]);  // {thr~/2, thr~/2}: the seed pair from one 4-B read
-    thb = splat2(tab[lk.th_off + ib]);
 #else
     tha = *reinterpret_cast<const f2v*>(tab + ia * P + RP);
     thb = *reinterpret_cast<const f2v*>(tab + ib * P + RP);
 #endif
-    (void)lk;
+    (void)lk;  // (the table's layout is static)
   } else {
     tha = thb = splat2(0.0f);
   }
@@ -791,8 +772,7 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
   Scalars& sc = *reinterpret_cast<Scalars*>(smem);            // 32 B reserved
   float* Cl = smem + 8;                                        // [K][CP] (signed rows: [2K+1])
   float2* El = reinterpret_cast<float2*>(Cl + (size_t)table_floats<RP, KIND>(K));  // [nbins]
-  Lik lks = lk;  // the C^T table's threshold column
-  lks.th_off = th_offset<RP, KIND>(K);
+
 
   // a wave = one slice of QSC_SLICE (32) pixel positions at a time, two lanes per pixel: lane
   // half h takes entries 2h, 2h+1 of every 4-entry chunk of the pixel's list; the halves'
@@ -894,7 +874,7 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_halves<RP, E, KIND, LOG>(c.src, ln.ent, 2 * QSC_SLICE, c.j1, c.buf, own, Cl, El, lks,
+    walk_halves<RP, E, KIND, LOG>(c.src, ln.ent, 2 * QSC_SLICE, c.j1, c.buf, own, Cl, El, lk,
                                   accp, nll);
     STAMP(w, 3 + 3 * i);
     // the two lane halves' partial dS: v_permlane32_swap (VALU) instead of an LDS shuffle
@@ -978,8 +958,7 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   float2* El = reinterpret_cast<float2*>(Sl + (size_t)table_floats<RP, KIND>(PT));  // [nbins]
   float* Pl = Sl + (size_t)table_floats<RP, KIND>(PT) + 2 * 256;  // [kCParts][R][64]
   (void)TR;
-  Lik lkc = lk;  // the S tile's threshold column
-  lkc.th_off = th_offset<RP, KIND>(PT);
+
   float* Nl = Pl + (size_t)kCParts * R * 64;                      // [kCParts]
   int t, ks;
   if (xcd_map) {
@@ -1039,9 +1018,9 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
   f2v nll = splat2(0.0f);
 #if QSC_CPASS_MASKED
-  walk_masked<RP, E, KIND, LOG>(src, lo, 64, j0, j0, j1, 1, buf, own, Sl, El, lkc, accp, nll);
+  walk_masked<RP, E, KIND, LOG>(src, lo, 64, j0, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
 #else
-  walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lkc, accp, nll);
+  walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
 #endif
   STAMP(wg, 2);
   const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
@@ -1106,8 +1085,7 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
   float2* El = reinterpret_cast<float2*>(Sl + (size_t)table_floats<RP, KIND>(PT));  // [nbins]
   float* Pl = Sl + (size_t)table_floats<RP, KIND>(PT) + 2 * 256;  // [U][R][64]   (NP > 1)
   (void)TR;
-  Lik lkc = lk;  // the S tile's threshold column
-  lkc.th_off = th_offset<RP, KIND>(PT);
+
   float* Nl = Pl + (NP > 1 ? (size_t)U * R * 64 : 0);             // [U] / [NW]
   const int t = blockIdx.x;
   const int Kp = nks * 64;
@@ -1165,7 +1143,7 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lkc, accp, nll);
+    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (NP == 1) {
       // the unit is the whole (tile, k-slice): its slab rows straight from registers
@@ -1219,13 +1197,11 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
 // pitch (floats) and row count of a gather table (sr: signed rows)
 inline int tpitch(int R, bool sr) {
   const int RP = R <= 4 ? 4 : (R <= 8 ? 8 : 16);
-  return ((sr && !QSC_SR_THTAB) || RP > 4) ? RP + 4 : 4;
+  return (sr || RP > 4) ? RP + 4 : 4;
 }
 inline size_t trows(int rows, bool sr) { return sr ? 2 * (size_t)rows + 1 : (size_t)rows; }
-// floats of a gather table (rows at the pitch, plus a separate threshold column if any)
-inline size_t tfloats(int rows, int R, bool sr) {
-  return trows(rows, sr) * tpitch(R, sr) + ((sr && QSC_SR_THTAB) ? trows(rows, sr) : 0);
-}
+// floats of a gather table
+inline size_t tfloats(int rows, int R, bool sr) { return trows(rows, sr) * tpitch(R, sr); }
 
 size_t cpass_tile_lds(int PT, int R, int nks, int NP, bool sr) {
   const size_t U = (size_t)nks * NP;
@@ -1272,9 +1248,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
   float2* El = reinterpret_cast<float2*>(Cl + (size_t)table_floats<RP, KIND>(K));  // [256]
   float* Sl = reinterpret_cast<float*>(El + 256);                   // [PT][CP] (signed: 2PT+1)
   float* Pl = Sl + (size_t)table_floats<RP, KIND>(PT);              // [U][R][64]  (NP > 1)
-  Lik lks = lk, lkc = lk;  // the threshold columns of C^T (S-step) and of the S tile (C-pass)
-  lks.th_off = th_offset<RP, KIND>(K);
-  lkc.th_off = th_offset<RP, KIND>(PT);
+
   const int NW = blockDim.x >> 6;
   const int U = nks * NP;
   float* Nl = Pl + (NP > 1 ? (size_t)U * R * 64 : 0);               // [max(U,16)]
@@ -1469,7 +1443,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_halves<RP, E, KIND, LOG>(c.src, ln.ent, 2 * QSC_SLICE, c.j1, c.buf, own, Cl, El, lks,
+    walk_halves<RP, E, KIND, LOG>(c.src, ln.ent, 2 * QSC_SLICE, c.j1, c.buf, own, Cl, El, lk,
                                   accp, nll);
     float acc[RP];
 #pragma unroll
@@ -1551,7 +1525,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lkc, accp, nll);
+    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (NP == 1) {
 #pragma unroll

@@ -14,7 +14,7 @@ i=0
 for rep in ${REPS:-1}; do
 for e in ${ENVS:--}; do
   i=$((i+1))
-  if [ "$e" = "-" ]; then ev=""; else ev="$e"; fi
+  if [ "$e" = "-" ]; then ev=""; else ev="${e//,/ }"; fi
   env $ev timeout -k 10 300 python bench.py --cpu-baseline 0 ${BENCH_ARGS} > $G/bench_$i.log 2>&1 || { tail -5 $G/bench_$i.log; exit 1; }
   tail -1 $G/bench_$i.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['kernels']; print('$e', round(d['value']), {x: round(v, 2) for x, v in k.items() if x.endswith('_us') and v})"
 done
