@@ -1,0 +1,93 @@
+"""Reconstruction-quality runs (SURVEY.md section 8(d) metric 2).
+
+Prints one JSON line of trajectories (map NMSE every few iterations, qmc/quantization_model.py
+:88-92, and the final SLF-NMSE, metrics.slf_nmse):
+
+  c2_free_s   BASELINE.md section 3 recipe at C2 (256 x 256 x 64, R = 4, one-bit probit, thr =
+              median, sigma = range/4, f = 0.1, S0, C0 = 0.5 rand, lambda = 100, lr 5e-3 / 1e-2):
+              the free-S solver of onebit_lowrank.ipynb :1230-1291 / qmc.ipynb :559-645 on the
+              fused launches, the bench's workload at C2 size; map NMSE at log-spaced iterations
+              and the best along the path (free S at ~6 one-bit samples per pixel over-fits);
+  c2_free_s_f05  the same map sampled at f = 0.5 (onebit_lowrank.ipynb's f).
+  c5_*        a generate_map-style radio map (maps.generate_map: Gaussian PSD bumps, path loss x
+              FFT-correlated log-normal shadowing, 256 x 256, K = 64, R = 4) quantized with the log
+              model as qmc/qmc.ipynb :537 does (4 log bins, LOG_OFFSET_4, sigma = 5), f = 0.1:
+                c5_dip       the DIP solver (dip.solve: decoder prior on S, C from zero), the
+                             notebook's C5 setting.
+
+  python tools/quality.py [--c2-iters 4000] [--dip-iters 600]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def traj(res, every):
+    return [[every * (i + 1), round(float(v), 5)] for i, v in enumerate(res.nmse)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--c2-iters", type=int, default=4000)
+    ap.add_argument("--dip-iters", type=int, default=600)
+    ap.add_argument("--seed", type=int, default=5)
+    args = ap.parse_args()
+    from quantized_spectrum_cartography_amd import dip, maps, metrics, qmc, synthetic
+    from quantized_spectrum_cartography_amd import quantization_model_log as qml
+    from quantized_spectrum_cartography_amd.utils import LOG_OFFSET_4, QUANTIZATION_BOUNDARIES_4_BINS_LOG
+    out = {}
+
+    # ---- C2 free S, BASELINE recipe (f = 0.1) and the same map sampled at f = 0.5 ----
+    I, J, K, R = synthetic.CONFIGS["c2"]
+    for name, f in (("c2_free_s", 0.1), ("c2_free_s_f05", 0.5)):
+        p = synthetic.onebit_problem(I, J, K, R, f=f, seed=20262)
+        marks = sorted({int(round(x / 10.0)) * 10 for x in np.geomspace(10, args.c2_iters, 14)})
+        t0 = time.perf_counter()
+        res = qmc.solve(p["Y"], p["Wx"], p["b"], p["sigma"], S_init=p["S0"], C_init=p["C0"],
+                        max_iter=args.c2_iters, use_graph=True, T_true=p["T_true"], nmse_every=10)
+        torch.cuda.synchronize()
+        tr = [[10 * (i + 1), round(float(v), 5)] for i, v in enumerate(res.nmse)]
+        best = min(tr, key=lambda x: x[1])
+        init = float(metrics.map_nmse(p["S0"].cuda(), p["C0"].cuda(), p["T_true"]))
+        out[name] = {"iters": args.c2_iters, "f": f, "wall_s": time.perf_counter() - t0,
+                     "map_nmse_init": init,
+                     "map_nmse": [x for x in tr if x[0] in marks],
+                     "map_nmse_best": best,
+                     "slf_nmse": metrics.slf_nmse(res.S, p["S_true"]),
+                     "cost_first": res.costs_s[0], "cost_last": res.costs_s[-1]}
+        print(json.dumps({name: [tr[-1], best]}), file=sys.stderr, flush=True)
+        del p, res
+
+    # ---- C5: generated map, log model ----
+    K, R, N = 64, 4, 256
+    m = maps.generate_map(K, R, shadow_sigma=5.0, Xc=50.0, I=N, J=N, seed=args.seed)
+    T, S_true = m["T"], m["S"]
+    torch.manual_seed(args.seed)
+    Y = qml.quantize(T.cpu(), 5.0, QUANTIZATION_BOUNDARIES_4_BINS_LOG, LOG_OFFSET_4).unsqueeze(1)
+    Wx = torch.bernoulli(torch.full((K, 1, N, N), 0.1))
+    b = QUANTIZATION_BOUNDARIES_4_BINS_LOG
+    out["c5_map"] = {"K": K, "R": R, "grid": [N, N], "f": 0.1, "model": "log, 4 bins",
+                     "sigma": 5.0, "offset": LOG_OFFSET_4,
+                     "bins_used": torch.bincount(Y.reshape(-1), minlength=4).tolist()}
+    if args.dip_iters:
+        every = max(1, args.dip_iters // 12)
+        t0 = time.perf_counter()
+        rd = dip.solve(Y, Wx, b, 5.0, R, offset=LOG_OFFSET_4, max_iter=args.dip_iters,
+                       T_true=T, nmse_every=every)
+        torch.cuda.synchronize()
+        out["c5_dip"] = {"iters": args.dip_iters, "wall_s": time.perf_counter() - t0,
+                         "map_nmse": traj(rd, every), "slf_nmse": metrics.slf_nmse(rd.S, S_true),
+                         "cost_first": rd.costs_s[0], "cost_last": rd.costs_s[-1]}
+        print(json.dumps({"c5_dip": out["c5_dip"]["map_nmse"][-1]}), file=sys.stderr, flush=True)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
