@@ -595,11 +595,21 @@ __device__ __forceinline__ float wave_sum_dpp(float x) {
   return ((a + b) + c) + d;
 }
 
-// x[l] + x[l ^ 32] in every lane (the same sum in both halves), through v_permlane32_swap
-__device__ __forceinline__ float half_sum(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
+// The S-step epilogue's lane-pair combine: a pixel's two lanes (l, l + 32) hold partial dS rows
+// x = elements 0..RH-1 and y = RH..RP-1 of the same pixel; one v_permlane32_swap exchanges x's
+// upper 32 lanes with y's lower ones, so lane l < 32 gets x[l] + x[l + 32] (its half's sums) and
+// lane l >= 32 y[l - 32] + y[l]: half_sum + pick of both in 2 VALU, the same sums in the same
+// order.  swap_lo: the value of x (lane < 32) or of y taken from the partner lane (lane >= 32):
+// the half-row selection of a row both lanes hold.
+__device__ __forceinline__ float half_sum_pick(float x, float y) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false,
                                                   false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap_lo(float x, float y) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false,
+                                                  false);
+  return __uint_as_float(r[0]);
 }
 
 // ||C||^2 in one fixed order (threads 0..255 stride 256, then the block sum): shared by the
@@ -616,13 +626,6 @@ __device__ __forceinline__ float cnorm_sq(const float* __restrict__ C, int n, fl
         if (i0 + 256 * j < n) s2 = __builtin_fmaf(v[j], v[j], s2);
     }
   return block_sum(s2, sh);
-}
-
-// a1 if odd else a0, as bit operations: a ternary on a lane-varying bit is turned into a
-// dynamically indexed register array (scratch) by the compiler
-__device__ __forceinline__ float pick(uint32_t oddmask, float a0, float a1) {
-  const uint32_t u0 = __float_as_uint(a0), u1 = __float_as_uint(a1);
-  return __uint_as_float(u0 ^ ((u0 ^ u1) & oddmask));
 }
 
 // N consecutive floats (N = 2, 4, 8) of a position-order row: 8/16-byte vector accesses
@@ -780,7 +783,6 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int p = lane & (QSC_SLICE - 1), h = lane >> 5;
-  const uint32_t hmask = 0u - (uint32_t)h;
   const int W = gridDim.x * kSWaves;
   const int w = blockIdx.x * kSWaves + wave;
   // Static slice schedule: wave w of W takes slices w, 2W-1-w, 2W+w, 4W-1-w, ... (snake order
@@ -881,8 +883,8 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     float acc[RP];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) {
-      acc[2 * j] = half_sum(accp[j].x);
-      acc[2 * j + 1] = half_sum(accp[j].y);
+      acc[2 * j] = accp[j].x;
+      acc[2 * j + 1] = accp[j].y;
     }
 
     // 5. epilogue: fused Adam on the lane's half row, or the raw gradient.  Padding rows
@@ -890,8 +892,8 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     float a[RH], pv[RH];
 #pragma unroll
     for (int j = 0; j < RH; ++j) {
-      a[j] = pick(hmask, acc[j], acc[RH + j]);
-      pv[j] = pick(hmask, sv[j], sv[RH + j]);
+      a[j] = half_sum_pick(acc[j], acc[RH + j]);
+      pv[j] = swap_lo(sv[j], sv[RH + j]);
     }
     if constexpr (ADAM) {
       float m[RH], v[RH];
@@ -1256,7 +1258,6 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
   const int Kp = nks * 64;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int p = lane & (QSC_SLICE - 1), h = lane >> 5;
-  const uint32_t hmask = 0u - (uint32_t)h;
   const float own_scale = own_scale_of<KIND, LOG>(lk);
   const int nsl = PT / QSC_SLICE;  // slices per tile
   // this wave's n-th slice of the tile (local index) and its global slice
@@ -1448,14 +1449,14 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
     float acc[RP];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) {
-      acc[2 * j] = half_sum(accp[j].x);
-      acc[2 * j + 1] = half_sum(accp[j].y);
+      acc[2 * j] = accp[j].x;
+      acc[2 * j + 1] = accp[j].y;
     }
     float a[RH], pv[RH], m[RH], v[RH];
 #pragma unroll
     for (int j = 0; j < RH; ++j) {
-      a[j] = pick(hmask, acc[j], acc[RH + j]);
-      pv[j] = pick(hmask, sv[j], sv[RH + j]);
+      a[j] = half_sum_pick(acc[j], acc[RH + j]);
+      pv[j] = swap_lo(sv[j], sv[RH + j]);
       m[j] = c.mv[j];
       v[j] = c.vv[j];
     }
