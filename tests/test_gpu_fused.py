@@ -372,3 +372,45 @@ def test_unobserved_p_underflow_is_a_deliberate_deviation():
     nll.backward()
     assert np.isfinite(nll.item())
     assert np.isfinite(Sg.grad.cpu().numpy()).all() and np.isfinite(Cg.grad.cpu().numpy()).all()
+
+
+# signed-row entries (include/qsc.h rowfmt 1) against the code-field form on the same inputs:
+# z~ = -z' exactly (sign-symmetric rounding), so S, C and the costs agree bit for bit
+@pytest.mark.parametrize("seed,R,I,J,K,tile", [(61, 8, 96, 80, 256, None), (62, 4, 64, 64, 64, 512),
+                                               (63, 3, 50, 70, 130, 256), (64, 16, 64, 64, 128, 512)])
+def test_signed_rows_match_code_field_entries(seed, R, I, J, K, tile):
+    from quantized_spectrum_cartography_amd import qmc
+    d = _random_case(seed, R, I, J, K)
+    res = {}
+    for fmt in (1, 0):
+        o = _obs(d["Y"], d["Wx"], d["b"], d["sigma"], R=R, tile=tile)
+        assert o.desc.rowfmt == 1, "the signed-row layout applies to these one-bit cases"
+        if fmt == 0:
+            o._fill(0)
+        r = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], S_init=d["S0"], C_init=d["C0"],
+                      max_iter=7, obs=o)
+        assert o.desc.rowfmt == fmt
+        res[fmt] = r
+    assert np.array_equal(res[0].S.cpu().numpy(), res[1].S.cpu().numpy())
+    assert np.array_equal(res[0].C.cpu().numpy(), res[1].C.cpu().numpy())
+    assert res[0].costs_c == res[1].costs_c and res[0].costs_s == res[1].costs_s
+
+
+def test_signed_rows_only_for_the_onebit_kind():
+    """rowfmt 1 only for the one-bit probit kind: the log model keeps code-field entries, the
+    predicate refuses the squared loss on a one-bit layout, and a pass engine for a model the
+    signed-row layout does not apply to re-packs it as code-field entries."""
+    from quantized_spectrum_cartography_amd import _lib
+    from quantized_spectrum_cartography_amd.fused import PassEngine
+    d = _random_case(65, 4, 32, 32, 64, nbins=4, log_model=True)
+    o = _obs(d["Y"], d["Wx"], d["b"], d["sigma"], offset=d["offset"], log_model=True, R=4)
+    assert o.desc.rowfmt == 0
+    d1 = _random_case(66, 4, 32, 32, 64)
+    o1 = _obs(d1["Y"], d1["Wx"], d1["b"], d1["sigma"], R=4)
+    assert o1.desc.rowfmt == 1
+    sq = _lib.make_model(d1["b"], d1["sigma"], 0.0, False, loss="squared")
+    assert _lib.lib().qsc_obs_signed_rows_ok(o1.desc, 4, o1.model) == 1
+    assert _lib.lib().qsc_obs_signed_rows_ok(o1.desc, 4, sq) == 0
+    o1.model = sq
+    PassEngine(o1, 4)
+    assert o1.desc.rowfmt == 0
