@@ -307,6 +307,36 @@ __device__ __forceinline__ f2v log2_2(f2v x) {
   return f2v{__builtin_amdgcn_logf(x.x), __builtin_amdgcn_logf(x.y)};
 }
 
+// Signed-row one-bit kind: z~ = s z' (the sign folded into the gathered row), so the tail side
+// is z~ < 0 for both codes (code 0: z' < 0; code 1: z' > 0) and g needs no sign flip, the row
+// being s*row.  Same arithmetic as the one-bit kind of lik_grad2, so the same P and g (but for
+// z' == 0 exactly, where T and 1 - T are both 1/2 to within the fit's 3e-7).  P itself is
+// returned: the walks take log2 of the product of two pairs' P (one v_log per 4 entries).
+__device__ __forceinline__ void onebit_sr_pg(f2v z, const Lik& c, f2v& P, f2v& g) {
+  const f2v u = f2v{__builtin_fabsf(z.x), __builtin_fabsf(z.y)};
+#if QSC_FTZ_SAT
+  const f2v E = exp2_2(fma2(-z, z, splat2(kMillsLogK - 101.0f)));
+#else
+  const f2v E = exp2_2(fma2(-z, z, splat2(kMillsLogK)));
+#endif
+  f2v N = u + splat2(kMillsN2);
+  N = fma2(N, u, splat2(kMillsN1));
+  N = fma2(N, u, splat2(kMillsN0));
+  f2v D = u + splat2(kMillsD3);
+  D = fma2(D, u, splat2(kMillsD2));
+  D = fma2(D, u, splat2(kMillsD1));
+  D = fma2(D, u, splat2(kMillsD0));
+#if QSC_FTZ_SAT
+  const f2v Ts = ((E * N) * rcp2(D)) * splat2(0x1p101f);
+#else
+  const f2v T = (E * N) * rcp2(D);
+  const f2v Ts = f2v{T.x < kMillsTsat ? 0.0f : T.x, T.y < kMillsTsat ? 0.0f : T.y};
+#endif
+  const f2v Q = splat2(1.0f) - Ts;
+  P = f2v{z.x < 0.0f ? Ts.x : Q.x, z.y < 0.0f ? Ts.y : Q.y};
+  g = (E * splat2(c.ob_kg)) * rcp2(P);
+}
+
 // lik_grad for two entries (t.x with code c0, t.y with code c1); log2P and g of -log P.
 // Linear general kind: the caller passes t in the SCALED form t' = -t / a (its register factor
 // vector pre-multiplied by -1/a, so the dot product yields t' directly) and edges pre-divided by
@@ -341,33 +371,8 @@ __device__ __forceinline__ void lik_grad2(f2v t, int c0, int c1, bool pa, bool p
     g = splat2(2.0f) * r * tinv;
     log2P = -(r * r) * splat2(kInvLn2);
   } else if (KIND == LIK_ONEBIT_SR) {
-    // z~ = s z' (the sign folded into the gathered row): the tail side is z~ < 0 for both codes
-    // (code 0: z' < 0; code 1: z' > 0) and g needs no sign flip, the row being s*row.  Same
-    // arithmetic as the one-bit kind below, so the same bits (but for z' == 0 exactly, where
-    // T and 1 - T are both 1/2 to within the fit's 3e-7)
-    const f2v z = t;
-    const f2v u = f2v{__builtin_fabsf(z.x), __builtin_fabsf(z.y)};
-#if QSC_FTZ_SAT
-    const f2v E = exp2_2(fma2(-z, z, splat2(kMillsLogK - 101.0f)));
-#else
-    const f2v E = exp2_2(fma2(-z, z, splat2(kMillsLogK)));
-#endif
-    f2v N = u + splat2(kMillsN2);
-    N = fma2(N, u, splat2(kMillsN1));
-    N = fma2(N, u, splat2(kMillsN0));
-    f2v D = u + splat2(kMillsD3);
-    D = fma2(D, u, splat2(kMillsD2));
-    D = fma2(D, u, splat2(kMillsD1));
-    D = fma2(D, u, splat2(kMillsD0));
-#if QSC_FTZ_SAT
-    const f2v Ts = ((E * N) * rcp2(D)) * splat2(0x1p101f);
-#else
-    const f2v T = (E * N) * rcp2(D);
-    const f2v Ts = f2v{T.x < kMillsTsat ? 0.0f : T.x, T.y < kMillsTsat ? 0.0f : T.y};
-#endif
-    const f2v Q = splat2(1.0f) - Ts;
-    const f2v P = f2v{z.x < 0.0f ? Ts.x : Q.x, z.y < 0.0f ? Ts.y : Q.y};
-    g = (E * splat2(c.ob_kg)) * rcp2(P);
+    f2v P;
+    onebit_sr_pg(t, c, P, g);
     log2P = log2_2(P);
     (void)c0;
     (void)c1;

@@ -288,7 +288,7 @@ __device__ __forceinline__ void pair_math(uint32_t ea, uint32_t eb, const f2v (&
                                           const f2v (&oa)[RP / 2], const f2v (&ob)[RP / 2],
                                           f2v tha, f2v thb,
                                           const float2* __restrict__ edges, const Lik& lk,
-                                          f2v (&acc)[RP / 2], f2v& nll, bool valid);
+                                          f2v (&acc)[RP / 2], f2v& nll, f2v& pq, bool valid);
 
 template <int RP, typename E, int KIND, bool LOG>
 __device__ __forceinline__ void pair_step(uint32_t ea, uint32_t eb, const f2v (&own)[RP / 2],
@@ -296,9 +296,10 @@ __device__ __forceinline__ void pair_step(uint32_t ea, uint32_t eb, const f2v (&
                                           const float2* __restrict__ edges, const Lik& lk,
                                           f2v (&acc)[RP / 2], f2v& nll, bool valid) {
   f2v oa[RP / 2], ob[RP / 2];
-  f2v tha, thb;
+  f2v tha, thb, pq;
   pair_rows<RP, E, KIND>(ea, eb, own, tab, oa, ob, tha, thb, lk);
-  pair_math<RP, E, KIND, LOG>(ea, eb, own, oa, ob, tha, thb, edges, lk, acc, nll, valid);
+  pair_math<RP, E, KIND, LOG>(ea, eb, own, oa, ob, tha, thb, edges, lk, acc, nll, pq, valid);
+  if constexpr (is_sr(KIND)) nll -= log2_2(pq);  // (single pair: the walks pair them up)
 }
 
 template <int RP, typename E, int KIND, bool LOG>
@@ -306,20 +307,23 @@ __device__ __forceinline__ void pair_math(uint32_t ea, uint32_t eb, const f2v (&
                                           const f2v (&oa)[RP / 2], const f2v (&ob)[RP / 2],
                                           f2v tha, f2v thb,
                                           const float2* __restrict__ edges, const Lik& lk,
-                                          f2v (&acc)[RP / 2], f2v& nll, bool valid) {
+                                          f2v (&acc)[RP / 2], f2v& nll, f2v& pq, bool valid) {
   using T = Ent<E>;
   if constexpr (is_sr(KIND)) {
     // signed rows: z~ = thr~ + own . row~ (both carry the entry's sign), no code / pad handling
     f2v t = f2v{dot2s<RP>(own, oa, tha), dot2s<RP>(own, ob, thb)};
     if (!valid) t = splat2(kPadZ);  // walk_masked's evaluations past a list end
-    f2v log2P, g;
+    // P goes to the caller (pq), which takes log2 of two pairs' product: the NLL costs one
+    // v_log per four entries (P >= 2^-25 or exactly 0, so four factors stay normal in fp32)
+    f2v g;
 #if QSC_DIAG_NOMATH
     g = t * splat2(1e-3f);
-    log2P = t;
+    pq = splat2(1.0f) + t * splat2(1e-30f);
 #else
-    lik_grad2<KIND, LOG>(t, 0, 0, false, false, edges, lk, log2P, g);
+    onebit_sr_pg(t, lk, pq, g);
 #endif
-    nll -= log2P;
+    (void)nll;
+    (void)edges;
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) acc[j] = fma2(splat2(g.x), oa[j], acc[j]);
 #pragma unroll
@@ -437,15 +441,21 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
         uint32_t e[4];
         Ent<E>::unpack(b[i], e);
         f2v xa[RP / 2], xb[RP / 2];
-        f2v txa, txb;
+        f2v txa, txb, pqa, pqb;
         pair_rows<RP, E, KIND>(e[2], e[3], own, tab, xa, xb, txa, txb, lk);
-        pair_math<RP, E, KIND, LOG>(e[0], e[1], own, ra, rb, tra, trb, edges, lk, acc, nll, true);
+        pair_math<RP, E, KIND, LOG>(e[0], e[1], own, ra, rb, tra, trb, edges, lk, acc, nll, pqa,
+                                    true);
         if (i + 1 < kGroup) {
           uint32_t f[4];
           Ent<E>::unpack(b[i + 1], f);
           pair_rows<RP, E, KIND>(f[0], f[1], own, tab, ra, rb, tra, trb, lk);
         }
-        pair_math<RP, E, KIND, LOG>(e[2], e[3], own, xa, xb, txa, txb, edges, lk, acc, nll, true);
+        pair_math<RP, E, KIND, LOG>(e[2], e[3], own, xa, xb, txa, txb, edges, lk, acc, nll, pqb,
+                                    true);
+        if constexpr (is_sr(KIND)) {
+          const f2v pp = pqa * pqb;
+          nll.x -= __builtin_amdgcn_logf(pp.x * pp.y);
+        }
       }
     if (!more) break;
 #pragma unroll
@@ -492,9 +502,36 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
     V2 nb[kGroupS];
 #pragma unroll
     for (int i = 0; i < kGroupS; ++i) nb[i] = ld_lane(src + (int64_t)min(jn + i, jlast) * row, lo);
+    if constexpr (is_sr(KIND)) {
+      // half chunks in pairs: one v_log of the four entries' product P
 #pragma unroll
-    for (int i = 0; i < kGroupS; ++i)
-      if (jb + i < j1) half_chunk<RP, E, KIND, LOG>(b[i], own, tab, edges, lk, acc, nll);
+      for (int i = 0; i < kGroupS; i += 2)
+        if (jb + i < j1) {
+          f2v pa, pb = splat2(1.0f);
+          {
+            uint32_t e[2];
+            Ent<E>::unpack2(b[i], e);
+            f2v oa[RP / 2], ob[RP / 2], tha, thb;
+            pair_rows<RP, E, KIND>(e[0], e[1], own, tab, oa, ob, tha, thb, lk);
+            pair_math<RP, E, KIND, LOG>(e[0], e[1], own, oa, ob, tha, thb, edges, lk, acc, nll,
+                                        pa, true);
+          }
+          if (jb + i + 1 < j1) {
+            uint32_t e[2];
+            Ent<E>::unpack2(b[i + 1], e);
+            f2v oa[RP / 2], ob[RP / 2], tha, thb;
+            pair_rows<RP, E, KIND>(e[0], e[1], own, tab, oa, ob, tha, thb, lk);
+            pair_math<RP, E, KIND, LOG>(e[0], e[1], own, oa, ob, tha, thb, edges, lk, acc, nll,
+                                        pb, true);
+          }
+          const f2v pp = pa * pb;
+          nll.x -= __builtin_amdgcn_logf(pp.x * pp.y);
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kGroupS; ++i)
+        if (jb + i < j1) half_chunk<RP, E, KIND, LOG>(b[i], own, tab, edges, lk, acc, nll);
+    }
     if (!more) break;
 #pragma unroll
     for (int i = 0; i < kGroupS; ++i) b[i] = nb[i];
