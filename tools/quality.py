@@ -82,8 +82,14 @@ def main():
         rd = dip.solve(Y, Wx, b, 5.0, R, offset=LOG_OFFSET_4, max_iter=args.dip_iters,
                        T_true=T, nmse_every=every)
         torch.cuda.synchronize()
+        zero = float(metrics.map_nmse(torch.zeros_like(rd.S), rd.C, T, log_offset=LOG_OFFSET_4))
         out["c5_dip"] = {"iters": args.dip_iters, "wall_s": time.perf_counter() - t0,
                          "map_nmse": traj(rd, every), "slf_nmse": metrics.slf_nmse(rd.S, S_true),
+                         # NMSE_LOG (qmc/quantization_model_log.py:104-111): the log-domain
+                         # error the log model is fitted in, vs the all-zero map's
+                         "map_nmse_log": float(metrics.map_nmse(rd.S, rd.C, T,
+                                                                log_offset=LOG_OFFSET_4)),
+                         "map_nmse_log_zero_map": zero,
                          "cost_first": rd.costs_s[0], "cost_last": rd.costs_s[-1]}
         print(json.dumps({"c5_dip": out["c5_dip"]["map_nmse"][-1]}), file=sys.stderr, flush=True)
     print(json.dumps(out), flush=True)
