@@ -52,6 +52,14 @@ constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 #ifndef QSC_ROW_PF_C
 #define QSC_ROW_PF_C 1
 #endif
+// fused launch at rank <= 8: waves per workgroup (16: 128 VGPRs each; 12: 168, 3 per SIMD) and
+// the software-pipelined S-step gather (signed rows), which needs the larger register budget
+#ifndef QSC_FUSED_WAVES
+#define QSC_FUSED_WAVES 16
+#endif
+#ifndef QSC_ROW_PF_S
+#define QSC_ROW_PF_S 0
+#endif
 // fused launch: C^T staged from 16-B reads; part-sum bins read at the start
 #ifndef QSC_CT_VEC
 #define QSC_CT_VEC 1
@@ -484,7 +492,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
 // read ahead unconditionally (clamped to the last row: static vmcnt accounting).
 constexpr int kGroupS = 8;
 
-template <int RP, typename E, int KIND, bool LOG>
+template <int RP, typename E, int KIND, bool LOG, bool PF = false>
 __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restrict__ src,
                                             uint32_t lo, int row, int j1,
                                             typename Ent<E>::V2 (&b)[kGroupS],
@@ -496,6 +504,56 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
   j1 = __builtin_amdgcn_readfirstlane(j1);
   const int jlast = max(j1 - 1, 0);
   int jb = 0;
+  if constexpr (PF && is_sr(KIND)) {
+    // software-pipelined gather (signed rows): the LDS rows of the next half chunk are read
+    // before the current one's arithmetic, so the gather latency runs under it.  Every buffered
+    // half chunk is a clamped, valid entry, so a read-ahead past the list end is harmless.
+    f2v ra[RP / 2], rb[RP / 2], tra, trb;
+    {
+      uint32_t e[2];
+      Ent<E>::unpack2(b[0], e);
+      pair_rows<RP, E, KIND>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
+    }
+    for (;;) {
+      const int jn = jb + kGroupS;
+      const bool more = jn < j1;
+      V2 nb[kGroupS];
+#pragma unroll
+      for (int i = 0; i < kGroupS; ++i)
+        nb[i] = ld_lane(src + (int64_t)min(jn + i, jlast) * row, lo);
+#pragma unroll
+      for (int i = 0; i < kGroupS; i += 2)
+        if (jb + i < j1) {
+          uint32_t e[2], f[2];
+          Ent<E>::unpack2(b[i], e);
+          Ent<E>::unpack2(b[i + 1], f);
+          f2v xa[RP / 2], xb[RP / 2], txa, txb, pa, pb = splat2(1.0f);
+          pair_rows<RP, E, KIND>(f[0], f[1], own, tab, xa, xb, txa, txb, lk);
+          pair_math<RP, E, KIND, LOG>(e[0], e[1], own, ra, rb, tra, trb, edges, lk, acc, nll, pa,
+                                      true);
+          if (i + 2 < kGroupS) {
+            uint32_t g[2];
+            Ent<E>::unpack2(b[i + 2], g);
+            pair_rows<RP, E, KIND>(g[0], g[1], own, tab, ra, rb, tra, trb, lk);
+          }
+          if (jb + i + 1 < j1)
+            pair_math<RP, E, KIND, LOG>(f[0], f[1], own, xa, xb, txa, txb, edges, lk, acc, nll,
+                                        pb, true);
+          const f2v pp = pa * pb;
+          nll.x -= __builtin_amdgcn_logf(pp.x * pp.y);
+        }
+      if (!more) break;
+#pragma unroll
+      for (int i = 0; i < kGroupS; ++i) b[i] = nb[i];
+      {
+        uint32_t e[2];
+        Ent<E>::unpack2(b[0], e);
+        pair_rows<RP, E, KIND>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
+      }
+      jb = jn;
+    }
+    return;
+  }
   for (;;) {
     const int jn = jb + kGroupS;
     const bool more = jn < j1;
@@ -1264,7 +1322,7 @@ size_t cpass_tile_lds(int PT, int R, int nks, int NP, bool sr) {
 // two slice register sets and 16-float rows need up to 256 VGPRs (2 waves per SIMD)
 template <int RP>
 struct FusedBlock {
-  static constexpr int v = RP > 8 ? 512 : 1024;
+  static constexpr int v = RP > 8 ? 512 : 64 * QSC_FUSED_WAVES;
 };
 
 template <int RP, typename E, int KIND, bool LOG>
@@ -1481,8 +1539,9 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_halves<RP, E, KIND, LOG>(c.src, ln.ent, 2 * QSC_SLICE, c.j1, c.buf, own, Cl, El, lk,
-                                  accp, nll);
+    walk_halves<RP, E, KIND, LOG, (QSC_ROW_PF_S != 0) && RP <= 8>(c.src, ln.ent, 2 * QSC_SLICE,
+                                                                   c.j1, c.buf, own, Cl, El, lk,
+                                                                   accp, nll);
     float acc[RP];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) {
@@ -2252,7 +2311,7 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
   // waves: two S-step slices each (the tile's nsl slices), 4..16 (4..8 at rank 16)
   const int nsl = d->PT / QSC_SLICE;
   const unsigned threads =
-      64u * (unsigned)std::min(RP > 8 ? 8 : 16, std::max(4, nsl / 2));
+      64u * (unsigned)std::min(RP > 8 ? 8 : QSC_FUSED_WAVES, std::max(4, nsl / 2));
   hipStream_t s = STREAM(stream);
 #define SCPASS_LAUNCH(RPV, ET, KD, LG)                                                         \
   do {                                                                                         \
