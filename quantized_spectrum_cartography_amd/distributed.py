@@ -52,6 +52,16 @@ def kslab_observations(Y_local, Wx_local, bin_boundaries, noise_std, dist, offse
                         log_model=log_model, tile=tile, R_hint=R_hint, count_hook=hook)
 
 
+
+def _capturable(dist):
+    """hipGraph capture of the iteration includes its collectives: RCCL ("nccl") can be
+    captured, gloo (CPU rehearsals of the sharded bench on one GPU) cannot, and a failed
+    capture leaves the stream unusable, so such process groups run eagerly from the start."""
+    try:
+        return dist.get_backend() == "nccl"
+    except (RuntimeError, ValueError, AttributeError):
+        return True
+
 class IJSlabSolver:
     """Free-S alternating solver on one pixel block per rank (see module docstring)."""
 
@@ -81,6 +91,9 @@ class IJSlabSolver:
         self.fuse = bool(fuse) and sup is not None and bool(sup())
         self._graphs = {}
         self.graph_tolerant, self.graph_error = True, None  # see qmc._capture
+        self.graph_capturable = _capturable(dist)
+        if not self.graph_capturable:
+            self.graph_error = "collectives over %s are not graph-capturable" % dist.get_backend()
 
     def fused_body(self):
         """S-step i + C-pass i+1 (one launch), then C-step i+1's exchange and update."""
@@ -168,6 +181,9 @@ class KSlabSolver:
         self.engine.init_state(self.S)
         self._graphs = {}
         self.graph_tolerant, self.graph_error = True, None  # see qmc._capture
+        self.graph_capturable = _capturable(dist)
+        if not self.graph_capturable:
+            self.graph_error = "collectives over %s are not graph-capturable" % dist.get_backend()
 
     def c_step(self):
         e = self.engine

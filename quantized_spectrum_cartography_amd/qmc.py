@@ -105,6 +105,8 @@ def _upload(g):
 def graph_for(solver, n):
     """The hipGraph of the exact kernel sequence of run(n) (captured once per n)."""
     graphs = solver.__dict__.setdefault("_graphs", {})
+    if getattr(solver, "graph_capturable", True) is False:
+        return None  # eager (the reason is in solver.graph_error)
     if n not in graphs:
         graphs[n] = _capture(solver, n, getattr(solver, "graph_tolerant", False))
     return graphs[n]
