@@ -257,13 +257,25 @@ struct Scalars {
 // is accumulated as a pair (summed by the caller).
 // the LDS rows of an entry pair (the gather half of pair_step)
 // (signed-row kind: the entry IS the row, whose float RP is the signed threshold -> tha/thb)
-template <int RP, typename E, int KIND>
+#ifndef QSC_DIAG_NOCONF_C
+#define QSC_DIAG_NOCONF_C 0
+#endif
+#ifndef QSC_DIAG_NOCONF_S
+#define QSC_DIAG_NOCONF_S 0
+#endif
+template <int RP, typename E, int KIND, int DG = 0>
 __device__ __forceinline__ void pair_rows(uint32_t ea, uint32_t eb, const f2v (&own)[RP / 2],
                                           const float* __restrict__ tab, f2v (&oa)[RP / 2],
                                           f2v (&ob)[RP / 2], f2v& tha, f2v& thb, const Lik& lk) {
   using T = Ent<E>;
   constexpr int P = TP<RP, KIND>::v;
-  const uint32_t ia = is_sr(KIND) ? ea : (ea & T::kMask), ib = is_sr(KIND) ? eb : (eb & T::kMask);
+  uint32_t ia = is_sr(KIND) ? ea : (ea & T::kMask), ib = is_sr(KIND) ? eb : (eb & T::kMask);
+  if constexpr (DG != 0) {
+    // diagnostic builds only (wrong values): every 16-lane group of a ds_read_b128 reads rows of
+    // 16 distinct residues mod 16, i.e. conflict-free gathers (bounds the bank-conflict cost)
+    ia = (ia & ~15u) | (threadIdx.x & 15u);
+    ib = (ib & ~15u) | (threadIdx.x & 15u);
+  }
 #if QSC_DIAG_NOLDS  // diagnostic build: no gather (bounds the LDS share of the pass)
 #pragma unroll
   for (int j = 0; j < RP / 2; ++j) {
@@ -434,7 +446,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
   {
     uint32_t e[4];
     Ent<E>::unpack(b[0], e);
-    pair_rows<RP, E, KIND>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
+    pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_C>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
   }
 #endif
   for (;;) {
@@ -450,13 +462,13 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
         Ent<E>::unpack(b[i], e);
         f2v xa[RP / 2], xb[RP / 2];
         f2v txa, txb, pqa, pqb;
-        pair_rows<RP, E, KIND>(e[2], e[3], own, tab, xa, xb, txa, txb, lk);
+        pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_C>(e[2], e[3], own, tab, xa, xb, txa, txb, lk);
         pair_math<RP, E, KIND, LOG>(e[0], e[1], own, ra, rb, tra, trb, edges, lk, acc, nll, pqa,
                                     true);
         if (i + 1 < kGroup) {
           uint32_t f[4];
           Ent<E>::unpack(b[i + 1], f);
-          pair_rows<RP, E, KIND>(f[0], f[1], own, tab, ra, rb, tra, trb, lk);
+          pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_C>(f[0], f[1], own, tab, ra, rb, tra, trb, lk);
         }
         pair_math<RP, E, KIND, LOG>(e[2], e[3], own, xa, xb, txa, txb, edges, lk, acc, nll, pqb,
                                     true);
@@ -471,7 +483,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
     {
       uint32_t e[4];
       Ent<E>::unpack(b[0], e);
-      pair_rows<RP, E, KIND>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
+      pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_C>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
     }
 #else
 #pragma unroll
@@ -512,7 +524,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
     {
       uint32_t e[2];
       Ent<E>::unpack2(b[0], e);
-      pair_rows<RP, E, KIND>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
+      pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_S>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
     }
     for (;;) {
       const int jn = jb + kGroupS;
@@ -528,13 +540,13 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
           Ent<E>::unpack2(b[i], e);
           Ent<E>::unpack2(b[i + 1], f);
           f2v xa[RP / 2], xb[RP / 2], txa, txb, pa, pb = splat2(1.0f);
-          pair_rows<RP, E, KIND>(f[0], f[1], own, tab, xa, xb, txa, txb, lk);
+          pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_S>(f[0], f[1], own, tab, xa, xb, txa, txb, lk);
           pair_math<RP, E, KIND, LOG>(e[0], e[1], own, ra, rb, tra, trb, edges, lk, acc, nll, pa,
                                       true);
           if (i + 2 < kGroupS) {
             uint32_t g[2];
             Ent<E>::unpack2(b[i + 2], g);
-            pair_rows<RP, E, KIND>(g[0], g[1], own, tab, ra, rb, tra, trb, lk);
+            pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_S>(g[0], g[1], own, tab, ra, rb, tra, trb, lk);
           }
           if (jb + i + 1 < j1)
             pair_math<RP, E, KIND, LOG>(f[0], f[1], own, xa, xb, txa, txb, edges, lk, acc, nll,
@@ -548,7 +560,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
       {
         uint32_t e[2];
         Ent<E>::unpack2(b[0], e);
-        pair_rows<RP, E, KIND>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
+        pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_S>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
       }
       jb = jn;
     }
@@ -570,7 +582,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
             uint32_t e[2];
             Ent<E>::unpack2(b[i], e);
             f2v oa[RP / 2], ob[RP / 2], tha, thb;
-            pair_rows<RP, E, KIND>(e[0], e[1], own, tab, oa, ob, tha, thb, lk);
+            pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_S>(e[0], e[1], own, tab, oa, ob, tha, thb, lk);
             pair_math<RP, E, KIND, LOG>(e[0], e[1], own, oa, ob, tha, thb, edges, lk, acc, nll,
                                         pa, true);
           }
@@ -578,7 +590,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
             uint32_t e[2];
             Ent<E>::unpack2(b[i + 1], e);
             f2v oa[RP / 2], ob[RP / 2], tha, thb;
-            pair_rows<RP, E, KIND>(e[0], e[1], own, tab, oa, ob, tha, thb, lk);
+            pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_S>(e[0], e[1], own, tab, oa, ob, tha, thb, lk);
             pair_math<RP, E, KIND, LOG>(e[0], e[1], own, oa, ob, tha, thb, edges, lk, acc, nll,
                                         pb, true);
           }

@@ -30,7 +30,7 @@ import torch
 
 from . import _lib
 from ._model import _dev
-from .qmc import issue_iterations, graph_for, run_iterations
+from .qmc import issue_iterations, prepare_iterations, run_iterations
 
 
 def kslab_bounds(K, world, rank):
@@ -123,7 +123,7 @@ class IJSlabSolver:
         issue_iterations(self, n)
 
     def prepare(self, n):
-        graph_for(self, n)
+        prepare_iterations(self, n)
 
     def run(self, n, use_graph=False):
         run_iterations(self, n, use_graph)
@@ -207,7 +207,7 @@ class KSlabSolver:
         issue_iterations(self, n)
 
     def prepare(self, n):
-        graph_for(self, n)
+        prepare_iterations(self, n)
 
     def run(self, n, use_graph=False):
         run_iterations(self, n, use_graph)

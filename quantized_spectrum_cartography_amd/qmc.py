@@ -59,21 +59,33 @@ def issue_iterations(solver, n):
 
 
 def _capture(solver, n, tolerant):
+    """Capture run(n)'s kernel sequence into a hipGraph on a side stream.
+
+    A capture that fails part-way (an engine error, an illegal synchronisation, a collective
+    that cannot be captured) is abandoned cleanly: any capture still open on the side stream or
+    the current stream is ended and its graph destroyed, and the device is synchronised, BEFORE
+    anything else is issued -- work issued onto a stream that is still capturing would be
+    recorded instead of run, and a collective there fails ("operation not permitted when stream
+    is capturing").  Then, for a tolerant solver, the failure is recorded in `graph_error`, the
+    solver is marked not capturable and runs eagerly from then on; otherwise the error is
+    re-raised.  If the capture cannot be ended the error is always raised."""
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
+    caller = torch.cuda.current_stream()
+    s.wait_stream(caller)
     try:
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
                 issue_iterations(solver, n)
-    except RuntimeError as e:
+    except Exception as e:  # noqa: BLE001 - every failure takes the same clean-up path
+        err = "%s: %s" % (type(e).__name__, e)
+        del g
+        abandon_capture((s, caller))  # raises if a capture stays open
         if not tolerant:
             raise
-        # sharded solvers: an RCCL build whose collectives cannot be captured (reported)
-        torch.cuda.synchronize()
-        solver.graph_error = "%s: %s" % (type(e).__name__, e)
-        warnings.warn("hipGraph capture failed; running eagerly (%s)" % solver.graph_error,
-                      RuntimeWarning)
+        solver.graph_error = err
+        solver.graph_capturable = False
+        warnings.warn("hipGraph capture failed; running eagerly (%s)" % err, RuntimeWarning)
         return None
     torch.cuda.current_stream().wait_stream(s)
     _upload(g)
@@ -83,18 +95,57 @@ def _capture(solver, n, tolerant):
 _hip = None
 
 
+def _hip_lib():
+    global _hip
+    if _hip is None:
+        import ctypes
+        h = ctypes.CDLL("libamdhip64.so")
+        h.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        h.hipGraphUpload.restype = ctypes.c_int
+        h.hipStreamIsCapturing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        h.hipStreamIsCapturing.restype = ctypes.c_int
+        h.hipStreamEndCapture.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
+        h.hipStreamEndCapture.restype = ctypes.c_int
+        h.hipGraphDestroy.argtypes = [ctypes.c_void_p]
+        h.hipGraphDestroy.restype = ctypes.c_int
+        h.hipGetLastError.argtypes = []
+        h.hipGetLastError.restype = ctypes.c_int
+        _hip = h
+    return _hip
+
+
+def stream_capture_status(stream):
+    """0 = not capturing, 1 = capture active, 2 = capture invalidated (hipStreamCaptureStatus)."""
+    import ctypes
+    st = ctypes.c_int(0)
+    rc = _hip_lib().hipStreamIsCapturing(ctypes.c_void_p(stream.cuda_stream), ctypes.byref(st))
+    return st.value if rc == 0 else -1  # -1: the query itself failed (treated as capturing)
+
+
+def abandon_capture(streams):
+    """End (and discard) any stream capture still open on `streams`, then synchronise the
+    device.  Raises RuntimeError if a capture cannot be ended."""
+    import ctypes
+    h = _hip_lib()
+    for st in streams:
+        if stream_capture_status(st) != 0:
+            graph = ctypes.c_void_p(None)
+            h.hipStreamEndCapture(ctypes.c_void_p(st.cuda_stream), ctypes.byref(graph))
+            if graph.value:
+                h.hipGraphDestroy(graph)
+    h.hipGetLastError()  # clear the (non-sticky) capture error
+    still = [st for st in streams if stream_capture_status(st) != 0]
+    if still:
+        raise RuntimeError("a failed hipGraph capture left %d stream(s) capturing" % len(still))
+    torch.cuda.synchronize()
+
+
 def _upload(g):
     """hipGraphUpload the instantiated graph now, so that its first replay does not pay the
     upload (a fixed ~tens of us that would otherwise land in a short timed run)."""
-    global _hip
     try:
-        if _hip is None:
-            import ctypes
-            _hip = ctypes.CDLL("libamdhip64.so")
-            _hip.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-            _hip.hipGraphUpload.restype = ctypes.c_int
         ex = g.raw_cuda_graph_exec()
-        rc = _hip.hipGraphUpload(ex, torch.cuda.current_stream().cuda_stream)
+        rc = _hip_lib().hipGraphUpload(ex, torch.cuda.current_stream().cuda_stream)
         if rc != 0:
             raise RuntimeError("hipGraphUpload returned %d" % rc)
         torch.cuda.current_stream().synchronize()
@@ -112,20 +163,35 @@ def graph_for(solver, n):
     return graphs[n]
 
 
+def graph_chunks(n):
+    """The graph lengths run(n) replays, in order: 1024-iteration chunks, then the remainder."""
+    out = []
+    while n > 0:
+        m = min(n, GRAPH_MAX_ITERS)
+        out.append(m)
+        n -= m
+    return out
+
+
+def prepare_iterations(solver, n):
+    """Capture (without executing) every graph that run(n, use_graph=True) will replay, so a
+    later timed run(n) captures, instantiates and uploads nothing."""
+    for m in sorted(set(graph_chunks(n))):
+        graph_for(solver, m)
+
+
 def run_iterations(solver, n, use_graph):
     """run(n): eager, or as replays of whole-run hipGraphs (one replay when n <= 1024), so the
     device work of a timed run(n) does not depend on how earlier runs were split."""
     if not (use_graph and torch.cuda.is_available() and solver.S.is_cuda):
         issue_iterations(solver, n)
         return
-    while n > 0:
-        m = min(n, GRAPH_MAX_ITERS)
+    for m in graph_chunks(n):
         g = graph_for(solver, m)
         if g is None:
             issue_iterations(solver, m)
         else:
             g.replay()
-        n -= m
 
 
 class FreeSSolver:
@@ -182,8 +248,8 @@ class FreeSSolver:
 
     def prepare(self, n):
         """Capture the kernel sequence of run(n) in a hipGraph now (capture executes nothing),
-        so that a later run(n, use_graph=True) is exactly one graph replay."""
-        graph_for(self, n)
+        so that a later run(n, use_graph=True) is graph replays only (one when n <= 1024)."""
+        prepare_iterations(self, n)
 
     def run(self, n, use_graph=False):
         run_iterations(self, n, use_graph)

@@ -1,0 +1,69 @@
+"""bench.py's multi-GPU launch logic (CPU): `python3 bench.py --gpus N` without WORLD_SIZE starts
+N ranks itself as a child torch.distributed.run job; as a rank it runs the bench."""
+import subprocess
+import sys
+
+import pytest
+
+import bench
+
+
+def _args(argv):
+    old = sys.argv
+    try:
+        sys.argv = ["bench.py"] + argv
+        return bench.parse()
+    finally:
+        sys.argv = old
+
+
+def test_single_gpu_runs_in_process():
+    assert bench.maybe_launch(_args([]), argv=[], env={}) is None
+    assert bench.maybe_launch(_args(["--gpus", "1"]), argv=["--gpus", "1"], env={}) is None
+
+
+def test_rank_process_does_not_relaunch():
+    a = _args(["--gpus", "8"])
+    assert bench.maybe_launch(a, argv=["--gpus", "8"], env={"WORLD_SIZE": "8"}) is None
+
+
+def test_plain_multi_gpu_command_spawns_torchrun(monkeypatch):
+    seen = {}
+
+    def fake_call(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return 7
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    argv = ["--gpus", "4", "--steps", "20", "--warmup", "5"]
+    rc = bench.maybe_launch(_args(argv), argv=argv, env={"HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    assert rc == 7  # the child's exit code is the bench's
+    cmd = seen["cmd"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd
+    assert "--master-addr=127.0.0.1" in cmd
+    assert any(c.startswith("--master-port=") for c in cmd)
+    i = cmd.index(bench.__file__.replace(".pyc", ".py")) if bench.__file__ in cmd else \
+        [j for j, c in enumerate(cmd) if c.endswith("bench.py")][0]
+    assert cmd[i + 1:] == argv  # the script's own arguments are forwarded unchanged
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_launcher_command_runs_this_script():
+    cmd = bench.launcher_cmd(["--gpus", "2"], 2, port=29999)
+    assert cmd[-3].endswith("bench.py") and cmd[-2:] == ["--gpus", "2"]
+    assert "--master-port=29999" in cmd
+
+
+def test_world_size_mismatch_exits_nonzero(monkeypatch):
+    """A process group whose size differs from --gpus never prints a bench line."""
+    monkeypatch.setattr(bench, "dist_init", lambda: (None, 0, 1))
+    monkeypatch.setattr(bench, "maybe_launch", lambda a: None)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    assert bench.main() == 2
+
+
+@pytest.mark.parametrize("steps", [20, 4096])
+def test_graph_chunks_cover_the_run(steps):
+    from quantized_spectrum_cartography_amd import qmc
+    ch = qmc.graph_chunks(steps // 2)
+    assert sum(ch) == steps // 2 and max(ch) <= qmc.GRAPH_MAX_ITERS
