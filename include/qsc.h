@@ -132,10 +132,16 @@ typedef struct qsc_state {
  *  wide   (wide == 1): uint32 entries, KBITS = QBITS = 24, code PAD = 255
  *  Signed-row entries (rowfmt == 1; one-bit linear model, narrow only, set by the caller between
  *  qsc_obs_layout and qsc_obs_fill when qsc_obs_signed_rows_ok): the value is the row of the
- *  pass's LDS table directly -- S-format  k + (code == 1 ? K : 0),  pad 2K;  C-format
- *  qlocal + (code == 1 ? PT : 0),  pad 2PT.  The passes stage each factor row twice, as
- *  [+row, +thr'] and [-row, -thr'] (thr' the scaled threshold), plus a neutral pad row, so an
- *  entry's code is applied by the gather itself (z of code 1 is -z of code 0, exactly). */
+ *  pass's LDS table directly -- with  Ko = round_up(K, 16), Qo = round_up(PT, 16):
+ *  S-format  k + (code == 1 ? Ko : 0),  pads 2Ko + r;  C-format  qlocal + (code == 1 ? Qo : 0),
+ *  pads 2Qo + r  (r in 0..15).  The passes stage each factor row twice, as [+row, +thr'] and
+ *  [-row, -thr'] (thr' the scaled threshold), plus 16 neutral pad rows, so an entry's code is
+ *  applied by the gather itself (z of code 1 is -z of code 0, exactly).
+ *  List order: qsc_obs_fill writes each list in ascending k / qlocal order with its pads last;
+ *  qsc_obs_schedule may then permute every list (and choose its pads' rows r) so that the lanes
+ *  of each 16-lane ds_read_b128 group read rows of distinct residues mod 16 at every slot --
+ *  bank-conflict-free gathers.  The passes accept either order (a list's order only changes the
+ *  order its gradient terms are summed in). */
 typedef struct qsc_obs_desc {
   int32_t K;      /* frequency bins in this (local) slab */
   int32_t P;      /* pixels I*J */
@@ -256,6 +262,22 @@ QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* desc, const i
                          const int32_t* s_width, const int64_t* s_off, const int32_t* c_width,
                          const int64_t* c_off, const int32_t* c_kmap, void* s_entries,
                          void* c_entries, void* stream);
+/* Bank-conflict-free list order (qsc_sched.cuh): re-orders the filled entries of both formats in
+ * place, per 16-lane group of a slice / (tile, k-slice) block, as an edge colouring of lanes x
+ * row residues (each slot holds each residue ceil(count / W) times at most, once whenever the
+ * group has <= W entries of that residue).  Blocks with lists longer than 256 keep their order.
+ * SYNCHRONOUS (reads the longest list width); run once per packing, after qsc_obs_fill. */
+QSC_API size_t qsc_obs_schedule_workspace_bytes(const qsc_obs_desc* desc);
+QSC_API int qsc_obs_schedule(const qsc_obs_desc* desc, const int32_t* s_width,
+                             const int64_t* s_off, const int32_t* c_width, const int64_t* c_off,
+                             void* s_entries, void* c_entries, void* ws, size_t ws_bytes,
+                             void* stream);
+/* Host (CPU) form of one group's schedule, the same code as the device pass (tests / tools):
+ * in/out are 16 lists of W uint32 entry values, lane-major; rowfmt/rows/wide describe the
+ * entry values as in qsc_obs_desc (rows = K for S-format lists, PT for C-format lists).
+ * Returns 0, or 1 when the group was copied unchanged (W > 256). */
+QSC_API int qsc_sched_lists_host(const uint32_t* in, uint32_t* out, int32_t W, int32_t rowfmt,
+                                 int32_t rows, int32_t wide);
 /* gather/scatter between natural pixel order [R][P] and position order [Pp][RP]
  * (RP = qsc_rank_pad(R); rows R..RP-1 and positions of no pixel are zero-filled / ignored) */
 QSC_API int qsc_perm_gather(const float* nat, const int32_t* perm, int32_t R, int32_t P,

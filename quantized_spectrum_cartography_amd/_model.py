@@ -42,6 +42,12 @@ def quantize(X, noise_std, bin_boundaries, offset=None, log_model=False, noise=N
     formed on the host with torch's log, binned on the GPU (qsc_bin_codes), see there.
     """
     out_dev = X.device
+    if log_model:
+        # the reference log model's default offset (qmc/quantization_model_log.py:7, :9)
+        from .utils import LOG_OFFSET_7_ADJUSTED
+        offset = LOG_OFFSET_7_ADJUSTED if offset is None else float(offset)
+        if not offset > 0.0:
+            raise ValueError("the log model needs offset > 0 (log(X + offset) at X = 0)")
     if noise is None:
         noise = torch.randn(X.shape)
     if log_model:

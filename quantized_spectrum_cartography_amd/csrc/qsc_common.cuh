@@ -480,6 +480,14 @@ __device__ __forceinline__ T block_sum(T v, T* sh) {
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 __host__ __device__ inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
 
+// Signed-row gather tables (include/qsc.h rowfmt 1) of `rows` factor rows: rows [0, rows) hold
+// [+row, +thr'], the negated copies start at row sr_off(rows), a multiple of 16 so that a row
+// and its negation share a bank residue (qsc_sched.cuh), then kSrPadRows neutral pad rows
+// 2 sr_off(rows) + r, one per residue r.
+constexpr int kSrPadRows = 16;
+__host__ __device__ inline int sr_off(int rows) { return (rows + 15) & ~15; }
+__host__ __device__ inline int sr_rows(int rows) { return 2 * sr_off(rows) + kSrPadRows; }
+
 // Position of row ql of C-format pixel tile t (include/qsc.h): whole slices dealt to the nt
 // tiles in snake order, so that every tile carries the same mix of the count-sorted positions.
 __host__ __device__ inline int64_t tile_pos(int t, int ql, int nt) {

@@ -9,7 +9,10 @@
 // count (stable sort) so the 64 lanes of a slice carry near-equal work.
 #include <hipcub/hipcub.hpp>
 
+#include <vector>
+
 #include "qsc_common.cuh"
+#include "qsc_sched.cuh"
 
 using namespace qsc;
 
@@ -115,17 +118,65 @@ __device__ __forceinline__ int64_t slot(int64_t base, int lanes, int lane, int j
 }
 
 // Entry values (include/qsc.h): code-field form  idx | code << KBITS  (pad: code PAD), or the
-// signed-row form (rowfmt 1)  idx + (code == 1 ? rows : 0)  (pad: row 2 * rows), where `rows` is
-// the table's row count, K for the S-format and PT for the C-format
+// signed-row form (rowfmt 1)  idx + (code == 1 ? sr_off(rows) : 0)  (pad: row 2 sr_off(rows)),
+// where `rows` is the table's row count, K for the S-format and PT for the C-format
 template <typename E>
 __device__ __forceinline__ E entry_of(uint32_t idx, uint32_t code, int sr, int rows) {
   using Tr = EntryTraits<E>;
-  return sr ? (E)(idx + (code == 1 ? (uint32_t)rows : 0u)) : (E)(idx | (code << Tr::kBits));
+  return sr ? (E)(idx + (code == 1 ? (uint32_t)sr_off(rows) : 0u)) : (E)(idx | (code << Tr::kBits));
 }
 template <typename E>
-__device__ __forceinline__ E pad_of(int sr, int rows) {
+__host__ __device__ __forceinline__ E pad_of(int sr, int rows) {
   using Tr = EntryTraits<E>;
-  return sr ? (E)(2u * (uint32_t)rows) : (E)(Tr::kPad << Tr::kBits);
+  return sr ? (E)(2u * (uint32_t)sr_off(rows)) : (E)(Tr::kPad << Tr::kBits);
+}
+template <typename E>
+__host__ __device__ __forceinline__ SchedFmt sched_fmt(int sr, int rows) {
+  SchedFmt f;
+  f.pad_base = (uint32_t)pad_of<E>(sr, rows);
+  f.rows = (uint32_t)rows;
+  f.sr = sr;
+  f.bits = EntryTraits<E>::kBits;
+  return f;
+}
+
+// Bank-conflict-free list order (qsc_sched.cuh), one wave per 16-lane group of one list block
+// (S-format: a slice's 32 position lists = 2 groups; C-format: a (tile, k-slice) block's 64 bin
+// lists = 4 groups), its scratch in LDS, worked by lane 0 (a serial edge colouring, run once
+// per packing).  `in` is a copy of the naturally ordered entries, `out` the packed array; blocks
+// of lists longer than Wcap keep their natural order.
+template <typename E>
+__global__ void __launch_bounds__(64) sched_kernel(const E* __restrict__ in, E* __restrict__ out,
+                                                   const int* __restrict__ width,
+                                                   const int64_t* __restrict__ off, int lanes,
+                                                   int Wcap, SchedFmt f) {
+  extern __shared__ __attribute__((aligned(16))) char scratch[];
+  const int groups = lanes / kSchedLanes;
+  const int li = blockIdx.x / groups, g = blockIdx.x - li * groups;
+  if (threadIdx.x != 0) return;
+  const int W = width[li];
+  const int64_t base = off[li];
+  auto slot = [&](int i, int j) -> int64_t {
+    return base + (int64_t)(j >> 2) * (lanes * 4) + b128_group_lane(g, i) * 4 + (j & 3);
+  };
+  auto get = [&](int i, int j) -> uint32_t { return (uint32_t)in[slot(i, j)]; };
+  auto put = [&](int i, int c, uint32_t v) { out[slot(i, c)] = (E)v; };
+  if (W <= Wcap && sched_group(scratch, W, f, get, put)) return;
+  for (int i = 0; i < kSchedLanes; ++i)
+    for (int j = 0; j < W; ++j) out[slot(i, j)] = in[slot(i, j)];
+}
+
+__global__ void width_max_kernel(const int* __restrict__ w, int n, int* __restrict__ out) {
+  __shared__ int sh[256];
+  int m = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) m = max(m, w[i]);
+  sh[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) sh[threadIdx.x] = max(sh[threadIdx.x], sh[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = sh[0];
 }
 
 // pad entries after the last list (read-ahead tail, QSC_ENTRY_TAIL)
@@ -337,10 +388,10 @@ QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* d, const int3
   if (!d || !codes || !perm || !s_width || !s_off || !c_width || !c_off || !c_kmap ||
       !s_entries || !c_entries || d->s_entries < QSC_ENTRY_TAIL || d->c_entries < QSC_ENTRY_TAIL)
     return QSC_EINVAL;
-  // signed rows: narrow entries, every row index (2K, 2PT) representable
+  // signed rows: narrow entries, every row index (up to the last pad row) representable
   const int sr = d->rowfmt == 1 ? 1 : 0;
-  if (d->rowfmt != 0 && (d->rowfmt != 1 || d->wide || 2 * (int64_t)d->K > 0xFFFF ||
-                         2 * (int64_t)d->PT > 0xFFFF || d->nbins != 2))
+  if (d->rowfmt != 0 && (d->rowfmt != 1 || d->wide || (int64_t)sr_rows(d->K) > 0x10000 ||
+                         (int64_t)sr_rows(d->PT) > 0x10000 || d->nbins != 2))
     return QSC_EINVAL;
   hipStream_t s = STREAM(stream);
   const dim3 tg((QSC_ENTRY_TAIL + kBlock - 1) / kBlock), tb(kBlock);
@@ -371,6 +422,69 @@ QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* d, const int3
   }
   QSC_CHECK_LAUNCH();
   return QSC_OK;
+}
+
+QSC_API size_t qsc_obs_schedule_workspace_bytes(const qsc_obs_desc* d) {
+  if (!d || d->s_entries < 0 || d->c_entries < 0) return 0;
+  const size_t eb = d->wide ? 4 : 2;
+  return align_up((size_t)std::max(d->s_entries, d->c_entries) * eb) + 256;
+}
+
+QSC_API int qsc_obs_schedule(const qsc_obs_desc* d, const int32_t* s_width, const int64_t* s_off,
+                             const int32_t* c_width, const int64_t* c_off, void* s_entries,
+                             void* c_entries, void* ws, size_t ws_bytes, void* stream) {
+  if (!d || !s_width || !s_off || !c_width || !c_off || !s_entries || !c_entries || !ws ||
+      ws_bytes < qsc_obs_schedule_workspace_bytes(d) || (d->rowfmt != 0 && d->rowfmt != 1))
+    return QSC_EINVAL;
+  hipStream_t s = STREAM(stream);
+  const size_t eb = d->wide ? 4 : 2;
+  char* copy = (char*)ws;
+  int* wmax = (int*)(copy + align_up((size_t)std::max(d->s_entries, d->c_entries) * eb));
+  const int sr = d->rowfmt == 1 ? 1 : 0;
+  for (int fmt = 0; fmt < 2; ++fmt) {
+    // fmt 0: S-format (slices of QSC_SLICE position lists, rows = K); 1: C-format (64 bin
+    // lists per (tile, k-slice) block, rows = PT)
+    const int nl = fmt == 0 ? d->Pp / QSC_SLICE : d->ntiles * d->nks;
+    const int lanes = fmt == 0 ? QSC_SLICE : 64;
+    const int rows = fmt == 0 ? d->K : d->PT;
+    const int* width = fmt == 0 ? s_width : c_width;
+    const int64_t* off = fmt == 0 ? s_off : c_off;
+    void* ent = fmt == 0 ? s_entries : c_entries;
+    const int64_t n = fmt == 0 ? d->s_entries : d->c_entries;
+    if (nl < 1 || n < 1) continue;
+    hipLaunchKernelGGL(width_max_kernel, dim3(1), dim3(256), 0, s, width, nl, wmax);
+    QSC_CHECK_LAUNCH();
+    int host_w = 0;
+    QSC_TRY(hipMemcpyAsync(&host_w, wmax, sizeof(int), hipMemcpyDeviceToHost, s));
+    QSC_TRY(hipStreamSynchronize(s));
+    const int wcap = std::min(host_w, kSchedMaxW);
+    if (wcap < 1) continue;
+    QSC_TRY(hipMemcpyAsync(copy, ent, (size_t)n * eb, hipMemcpyDeviceToDevice, s));
+    const dim3 grid((unsigned)((int64_t)nl * (lanes / kSchedLanes)));
+    const size_t shm = sched_scratch_bytes(wcap);
+    if (d->wide)
+      hipLaunchKernelGGL(sched_kernel<uint32_t>, grid, dim3(64), shm, s, (const uint32_t*)copy,
+                         (uint32_t*)ent, width, off, lanes, wcap, sched_fmt<uint32_t>(0, rows));
+    else
+      hipLaunchKernelGGL(sched_kernel<uint16_t>, grid, dim3(64), shm, s, (const uint16_t*)copy,
+                         (uint16_t*)ent, width, off, lanes, wcap, sched_fmt<uint16_t>(sr, rows));
+    QSC_CHECK_LAUNCH();
+  }
+  return QSC_OK;
+}
+
+QSC_API int qsc_sched_lists_host(const uint32_t* in, uint32_t* out, int32_t W, int32_t rowfmt,
+                                 int32_t rows, int32_t wide) {
+  if (!in || !out || W < 0 || rows < 1 || (rowfmt != 0 && rowfmt != 1) || (rowfmt && wide))
+    return QSC_EINVAL;
+  const SchedFmt f = wide ? sched_fmt<uint32_t>(0, rows) : sched_fmt<uint16_t>(rowfmt, rows);
+  if (W == 0) return QSC_OK;
+  std::vector<unsigned char> scratch(sched_scratch_bytes(W) + 16);
+  auto get = [&](int i, int j) -> uint32_t { return in[(size_t)i * W + j]; };
+  auto put = [&](int i, int c, uint32_t v) { out[(size_t)i * W + c] = v; };
+  if (sched_group(scratch.data(), W, f, get, put)) return QSC_OK;
+  for (size_t i = 0; i < (size_t)kSchedLanes * W; ++i) out[i] = in[i];
+  return 1;  // kept the natural order (W > kSchedMaxW)
 }
 
 }  // extern "C"

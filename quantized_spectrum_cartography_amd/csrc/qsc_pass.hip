@@ -100,44 +100,47 @@ struct TP {
   static constexpr int v = KIND == LIK_ONEBIT_SR ? RP + 4 : Pitch<RP>::v;
 };
 constexpr bool is_sr(int kind) { return kind == LIK_ONEBIT_SR; }
-// rows of a table: K (C^T) or PT (S tile), or 2 * rows + 1 with signed rows
+// rows of a table: K (C^T) or PT (S tile), or sr_rows(rows) with signed rows (qsc_common.cuh)
 template <int KIND>
 __device__ __host__ __forceinline__ int table_rows(int rows) {
-  return is_sr(KIND) ? 2 * rows + 1 : rows;
+  return is_sr(KIND) ? sr_rows(rows) : rows;
 }
 // floats of a gather table of `rows` rows
 template <int RP, int KIND>
 __device__ __host__ __forceinline__ int table_floats(int rows) {
   return table_rows<KIND>(rows) * TP<RP, KIND>::v;
 }
-// the signed thresholds of rows i (+thr~) and rows + i (-thr~) of a signed-row table
+// the signed thresholds of rows i (+thr~) and sr_off(rows) + i (-thr~) of a signed-row table
 template <int RP, int KIND>
 __device__ __forceinline__ void put_th(float* tab, int rows, int i, float th) {
   constexpr int P = TP<RP, KIND>::v;
   *reinterpret_cast<float2*>(tab + i * P + RP) = make_float2(th, 0.0f);
-  *reinterpret_cast<float2*>(tab + (rows + i) * P + RP) = make_float2(-th, 0.0f);
+  *reinterpret_cast<float2*>(tab + (sr_off(rows) + i) * P + RP) = make_float2(-th, 0.0f);
 }
 // row i of a gather table from 4-float groups v[0..RP): signed-row tables also get the threshold
-// in float RP and the negated copy at row rows + i
+// in float RP and the negated copy at row sr_off(rows) + i
 template <int RP, int KIND>
 __device__ __forceinline__ void put_row4(float* tab, int rows, int i, int r, const float4& v,
                                          float th) {
   constexpr int P = TP<RP, KIND>::v;
   *reinterpret_cast<float4*>(tab + i * P + r) = v;
   if constexpr (is_sr(KIND)) {
-    *reinterpret_cast<float4*>(tab + (rows + i) * P + r) = make_float4(-v.x, -v.y, -v.z, -v.w);
+    *reinterpret_cast<float4*>(tab + (sr_off(rows) + i) * P + r) =
+        make_float4(-v.x, -v.y, -v.z, -v.w);
     if (r == 0) put_th<RP, KIND>(tab, rows, i, th);
   }
 }
-// the neutral pad row 2 * rows of a signed-row table ([0, kPadZ]: P == 1, g == 0 exactly)
+// the kSrPadRows neutral pad rows 2 sr_off(rows) + r of a signed-row table ([0, kPadZ]: P == 1,
+// g == 0 exactly), one per bank residue r (the scheduled pads of qsc_sched.cuh)
 template <int RP, int KIND>
 __device__ __forceinline__ void put_pad_row(float* tab, int rows) {
   if constexpr (is_sr(KIND)) {
     constexpr int P = TP<RP, KIND>::v;
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < kSrPadRows) {
+      float* row = tab + (2 * sr_off(rows) + (int)threadIdx.x) * P;
 #pragma unroll
-      for (int r = 0; r < RP; ++r) tab[2 * rows * P + r] = 0.0f;
-      *reinterpret_cast<float2*>(tab + 2 * rows * P + RP) = make_float2(kPadZ, 0.0f);
+      for (int r = 0; r < RP; ++r) row[r] = 0.0f;
+      *reinterpret_cast<float2*>(row + RP) = make_float2(kPadZ, 0.0f);
     }
   }
 }
@@ -1308,7 +1311,7 @@ inline int tpitch(int R, bool sr) {
   const int RP = R <= 4 ? 4 : (R <= 8 ? 8 : 16);
   return (sr || RP > 4) ? RP + 4 : 4;
 }
-inline size_t trows(int rows, bool sr) { return sr ? 2 * (size_t)rows + 1 : (size_t)rows; }
+inline size_t trows(int rows, bool sr) { return sr ? (size_t)sr_rows(rows) : (size_t)rows; }
 // floats of a gather table
 inline size_t tfloats(int rows, int R, bool sr) { return trows(rows, sr) * tpitch(R, sr); }
 
@@ -1433,6 +1436,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
   auto stage = [&]() {
 #if QSC_CT_VEC
     if (cvec) {
+      const int Ko = sr_off(K);  // the negated half of a signed-row C^T table
       auto put = [&](int i, const float4& v) {
         const int f = 4 * i, r = f / K, k = f - r * K;
         Cl[k * CP + r] = v.x;
@@ -1440,10 +1444,10 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
         Cl[(k + 2) * CP + r] = v.z;
         Cl[(k + 3) * CP + r] = v.w;
         if constexpr (is_sr(KIND)) {
-          Cl[(K + k) * CP + r] = -v.x;
-          Cl[(K + k + 1) * CP + r] = -v.y;
-          Cl[(K + k + 2) * CP + r] = -v.z;
-          Cl[(K + k + 3) * CP + r] = -v.w;
+          Cl[(Ko + k) * CP + r] = -v.x;
+          Cl[(Ko + k + 1) * CP + r] = -v.y;
+          Cl[(Ko + k + 2) * CP + r] = -v.z;
+          Cl[(Ko + k + 3) * CP + r] = -v.w;
         }
       };
       if (k0 < n4) put(k0, cq);
@@ -1452,7 +1456,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
       for (int i = k0; i < K * (RP - R); i += blockDim.x) {  // rows R..RP-1 are zero
         const int k = i / (RP - R), r = R + (i - k * (RP - R));
         Cl[k * CP + r] = 0.0f;
-        if constexpr (is_sr(KIND)) Cl[(K + k) * CP + r] = -0.0f;
+        if constexpr (is_sr(KIND)) Cl[(Ko + k) * CP + r] = -0.0f;
       }
       if constexpr (is_sr(KIND))
         for (int k = k0; k < K; k += blockDim.x) put_th<RP, KIND>(Cl, K, k, lk.ob_thr);
@@ -1578,7 +1582,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
       float nv[RH];
 #pragma unroll
       for (int j = 0; j < RH; ++j) nv[j] = -pv[j];
-      st_row<RH>(Sl + (PT + il * QSC_SLICE + p) * CP + h * RH, nv);
+      st_row<RH>(Sl + (sr_off(PT) + il * QSC_SLICE + p) * CP + h * RH, nv);
     }
     nsq = wave_sum_dpp(nsq);
     if (lane == 0) part_nsq_s[s] = nsq;
@@ -2262,7 +2266,8 @@ static bool scpass_fits(const qsc_obs_desc* d, int R, bool sr) {
 // LDS (the S-pass at its resident-block count; the C-pass tile form or, where that does not
 // apply, the per-slice form; the fused launch where it applies)
 static bool sr_layout_ok(const qsc_obs_desc* d, int R) {
-  if (d->wide || d->nbins != 2 || 2 * (int64_t)d->K > 0xFFFF || 2 * (int64_t)d->PT > 0xFFFF)
+  if (d->wide || d->nbins != 2 || (int64_t)sr_rows(d->K) > 0x10000 ||
+      (int64_t)sr_rows(d->PT) > 0x10000)
     return false;
   const int RP = rp_of(R);
   if (spass_lds(d, R, true) * spass_bpc(RP) > 160 * 1024) return false;

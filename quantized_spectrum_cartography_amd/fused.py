@@ -25,9 +25,10 @@ class PassEngine:
         if not 1 <= R <= _lib.QSC_MAX_R:
             raise ValueError("rank R must be in [1, %d]" % _lib.QSC_MAX_R)
         self.obs, self.R = obs, R
-        obs.ensure_rank(R)
+        # the packed entries at this rank (signed rows, or a code-field copy: obs.layout)
+        self.desc, self.s_entries, self.c_entries = obs.layout(R)
         dev = obs.device
-        nb = _lib.lib().qsc_pass_workspace_bytes(obs.desc, R)
+        nb = _lib.lib().qsc_pass_workspace_bytes(self.desc, R)
         if nb == 0:
             raise _lib.QscError("invalid observation descriptor")
         # zeroed once: the S-pass keeps its slice scheduler words in the workspace and leaves
@@ -52,40 +53,40 @@ class PassEngine:
     # ---- passes -------------------------------------------------------------------------
     def cpass(self, S_pos, C):
         o = self.obs
-        _lib.call("qsc_cpass", o.desc, _lib.ptr(o.c_entries), _lib.ptr(o.c_width), _lib.ptr(o.c_off),
+        _lib.call("qsc_cpass", self.desc, _lib.ptr(self.c_entries), _lib.ptr(o.c_width), _lib.ptr(o.c_off),
                   _lib.ptr(o.c_kmap), o.model, self.R, _lib.ptr(S_pos), _lib.ptr(C),
                   _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
 
     def cfinish(self, C, mode, dC=None, mC=None, vC=None, adam=None, lambda_c=0.0,
                 normsq_ext=None, record=True):
         hist, cap = (self.hist, self.hist_cap) if (record and self.hist_cap) else (None, 0)
-        _lib.call("qsc_cfinish", self.obs.desc, self.R, _lib.ptr(C), int(mode), _lib.ptr(dC),
+        _lib.call("qsc_cfinish", self.desc, self.R, _lib.ptr(C), int(mode), _lib.ptr(dC),
                   _lib.ptr(mC), _lib.ptr(vC), adam, float(lambda_c), _lib.ptr(normsq_ext),
                   _lib.ptr(self.state), _lib.ptr(hist), cap, _lib.ptr(self.ws), self.ws.numel(),
                   _lib.stream())
 
     def spass(self, S_pos, C, mode, dS=None, mS=None, vS=None, adam=None, lambda_s=0.0):
         o = self.obs
-        _lib.call("qsc_spass", o.desc, _lib.ptr(o.s_entries), _lib.ptr(o.s_width), _lib.ptr(o.s_off),
+        _lib.call("qsc_spass", self.desc, _lib.ptr(self.s_entries), _lib.ptr(o.s_width), _lib.ptr(o.s_off),
                   o.model, self.R, _lib.ptr(S_pos), _lib.ptr(C), int(mode), _lib.ptr(dS),
                   _lib.ptr(mS), _lib.ptr(vS), adam, float(lambda_s), _lib.ptr(self.state),
                   _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
 
     def scpass_supported(self):
-        return bool(_lib.lib().qsc_scpass_supported(self.obs.desc, self.R))
+        return bool(_lib.lib().qsc_scpass_supported(self.desc, self.R))
 
     def scpass(self, S_pos, C, mS, vS, adam, lambda_s):
         """spass (mode 1, Adam) fused with the next cpass at the updated S (qsc_scpass)."""
         o = self.obs
-        _lib.call("qsc_scpass", o.desc, _lib.ptr(o.s_entries), _lib.ptr(o.s_width),
-                  _lib.ptr(o.s_off), _lib.ptr(o.c_entries), _lib.ptr(o.c_width),
+        _lib.call("qsc_scpass", self.desc, _lib.ptr(self.s_entries), _lib.ptr(o.s_width),
+                  _lib.ptr(o.s_off), _lib.ptr(self.c_entries), _lib.ptr(o.c_width),
                   _lib.ptr(o.c_off), _lib.ptr(o.c_kmap), o.model, self.R, _lib.ptr(S_pos),
                   _lib.ptr(C), _lib.ptr(mS),
                   _lib.ptr(vS), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),
                   self.ws.numel(), _lib.stream())
 
     def supdate(self, S_pos, mS, vS, g, adam, lambda_s):
-        _lib.call("qsc_supdate", self.obs.desc, self.R, _lib.ptr(S_pos), _lib.ptr(mS), _lib.ptr(vS),
+        _lib.call("qsc_supdate", self.desc, self.R, _lib.ptr(S_pos), _lib.ptr(mS), _lib.ptr(vS),
                   _lib.ptr(g), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),
                   self.ws.numel(), _lib.stream())
 
@@ -101,7 +102,7 @@ class PassEngine:
 
     def flush(self, record=True):
         hist, cap = (self.hist, self.hist_cap) if (record and self.hist_cap) else (None, 0)
-        _lib.call("qsc_state_flush", self.obs.desc, self.R, _lib.ptr(self.state), _lib.ptr(hist),
+        _lib.call("qsc_state_flush", self.desc, self.R, _lib.ptr(self.state), _lib.ptr(hist),
                   cap, _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
 
     # ---- composite ----------------------------------------------------------------------

@@ -14,6 +14,12 @@ from . import _lib
 from ._model import _dev, _ws
 
 
+def ctypes_copy(dst, src):
+    """Field-by-field copy of a ctypes Structure."""
+    for name, _ in src._fields_:
+        setattr(dst, name, getattr(src, name))
+
+
 def default_tile(P, R, K):
     """C-pass pixel tile (positions, a power of two in [128, 1024]).
 
@@ -50,13 +56,18 @@ class Observations:
       tile: optional C-pass tile size (positions, multiple of 64).
       loss: "probit" (the likelihood of qmc/qmc.ipynb) or "squared" (the Euclidean criterion
             ||Wx (T_hat - Obs)||^2 of qmc/qmc_dowjons.ipynb :142, Obs the bin midpoints).
+      schedule: order every packed list for bank-conflict-free LDS gathers (qsc_obs_schedule;
+            default on, QSC_SCHEDULE=0 turns it off).  Results change only by summation order.
     """
 
     def __init__(self, Y, Wx, bin_boundaries, noise_std, offset=0.0, log_model=False, perm=None,
-                 tile=None, R_hint=8, count_hook=None, loss="probit"):
+                 tile=None, R_hint=8, count_hook=None, loss="probit", schedule=None):
         K = Y.shape[0]
         I, J = Y.shape[-2], Y.shape[-1]
         P = I * J
+        if schedule is None:  # QSC_SCHEDULE=0: natural list order (A/B switch)
+            schedule = os.environ.get("QSC_SCHEDULE", "1") != "0"
+        self.schedule = bool(schedule)
         self.K, self.I, self.J, self.P = K, I, J, P
         PT = int(tile or default_tile(P, R_hint, K))
         if PT < 64 or PT % 64:
@@ -122,23 +133,49 @@ class Observations:
         # through the gathered row) wherever the passes' doubled tables fit at this rank
         self._fill(1 if self.signed_rows_ok(R_hint) else 0)
 
-    def _fill(self, rowfmt):
-        self.desc.rowfmt = int(rowfmt)
-        _lib.call("qsc_obs_fill", _lib.ptr(self.codes), self.desc, _lib.ptr(self.perm),
+    def _fill(self, rowfmt, desc=None, s_entries=None, c_entries=None):
+        """Pack the entries in format `rowfmt` into (desc, s_entries, c_entries) (default: this
+        object's own arrays; only before any pass engine uses them, see layout())."""
+        if desc is None:
+            if getattr(self, "_engines", 0):
+                raise RuntimeError("the packed entries are in use by a pass engine (and maybe a "
+                                   "captured hipGraph): re-packing them in place is refused")
+            desc, s_entries, c_entries = self.desc, self.s_entries, self.c_entries
+        desc.rowfmt = int(rowfmt)
+        _lib.call("qsc_obs_fill", _lib.ptr(self.codes), desc, _lib.ptr(self.perm),
                   _lib.ptr(self.s_width), _lib.ptr(self.s_off), _lib.ptr(self.c_width),
-                  _lib.ptr(self.c_off), _lib.ptr(self.c_kmap), _lib.ptr(self.s_entries),
-                  _lib.ptr(self.c_entries), _lib.stream())
+                  _lib.ptr(self.c_off), _lib.ptr(self.c_kmap), _lib.ptr(s_entries),
+                  _lib.ptr(c_entries), _lib.stream())
+        if self.schedule:
+            # bank-conflict-free list order (include/qsc.h qsc_obs_schedule): the same order for
+            # both entry formats (it depends only on the row residues), so their results agree
+            ws = _ws(_lib.lib().qsc_obs_schedule_workspace_bytes(desc), self.device)
+            _lib.call("qsc_obs_schedule", desc, _lib.ptr(self.s_width), _lib.ptr(self.s_off),
+                      _lib.ptr(self.c_width), _lib.ptr(self.c_off), _lib.ptr(s_entries),
+                      _lib.ptr(c_entries), _lib.ptr(ws), ws.numel(), _lib.stream())
 
     def signed_rows_ok(self, R):
         if os.environ.get("QSC_SIGNED_ROWS", "1") == "0":  # A/B switch (tuning runs)
             return False
         return bool(_lib.lib().qsc_obs_signed_rows_ok(self.desc, int(R), self.model))
 
-    def ensure_rank(self, R):
-        """Re-pack in the code-field format if the signed-row layout chosen for R_hint does not
-        apply at rank R (the entry count is the same; only the values change)."""
-        if self.desc.rowfmt == 1 and not self.signed_rows_ok(R):
-            self._fill(0)
+    def layout(self, R):
+        """(desc, s_entries, c_entries) the passes read at rank R.  The signed-row packing chosen
+        for R_hint is used where it applies at R; otherwise a code-field copy is packed once and
+        kept (same entry count, other values).  The shared packing is never re-packed in place,
+        so hipGraphs captured by other solvers on this object stay valid (their kernels hold the
+        descriptor and entry pointers by value)."""
+        self._engines = getattr(self, "_engines", 0) + 1
+        if self.desc.rowfmt != 1 or self.signed_rows_ok(R):
+            return self.desc, self.s_entries, self.c_entries
+        if getattr(self, "_code_field", None) is None:
+            d = _lib.QscObsDesc()
+            ctypes_copy(d, self.desc)
+            s_e = torch.empty_like(self.s_entries)
+            c_e = torch.empty_like(self.c_entries)
+            self._fill(0, d, s_e, c_e)
+            self._code_field = (d, s_e, c_e)
+        return self._code_field
 
     # ---- info -----------------------------------------------------------------------
     @property

@@ -414,5 +414,33 @@ def test_signed_rows_only_for_the_onebit_kind():
     assert _lib.lib().qsc_obs_signed_rows_ok(o1.desc, 4, o1.model) == 1
     assert _lib.lib().qsc_obs_signed_rows_ok(o1.desc, 4, sq) == 0
     o1.model = sq
-    PassEngine(o1, 4)
-    assert o1.desc.rowfmt == 0
+    e = PassEngine(o1, 4)
+    assert e.desc.rowfmt == 0          # the engine reads a code-field copy ...
+    assert o1.desc.rowfmt == 1         # ... the shared signed-row packing is left alone
+    assert e.s_entries.data_ptr() != o1.s_entries.data_ptr()
+
+
+def test_other_rank_engine_does_not_invalidate_captured_graph():
+    """A solver's hipGraph captured on a signed-row layout stays correct after an engine at a
+    rank whose tables do not fit signed rows is built on the same Observations (ADVICE r2:
+    the shared packing used to be re-packed in place under the captured graph)."""
+    from quantized_spectrum_cartography_amd.fused import PassEngine
+    from quantized_spectrum_cartography_amd.qmc import FreeSSolver
+    d = _random_case(67, 4, 64, 64, 64)
+    o = _obs(d["Y"], d["Wx"], d["b"], d["sigma"], R=4, tile=512)
+    assert o.desc.rowfmt == 1
+    ref = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32)
+    ref.run(6, use_graph=False)
+    sol = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32)
+    sol.prepare(3)
+    sol.run(3, use_graph=True)
+    # an engine whose model the signed rows do not apply to (as a rank too large would)
+    from quantized_spectrum_cartography_amd import _lib
+    keep = o.model
+    o.model = _lib.make_model(d["b"], d["sigma"], 0.0, False, loss="squared")
+    PassEngine(o, 4)
+    o.model = keep
+    assert o.desc.rowfmt == 1
+    sol.run(3, use_graph=True)  # replays the graph captured before
+    assert np.array_equal(ref.S.cpu().numpy(), sol.S.cpu().numpy())
+    assert np.array_equal(ref.C.cpu().numpy(), sol.C.cpu().numpy())

@@ -165,3 +165,17 @@ def test_fused_erf_matches_ocml():
 def test_fails_loudly_on_bad_rank(qm):
     with pytest.raises(ValueError):
         qm.get_tensor(torch.rand(17, 1, 4, 4).cuda(), torch.rand(17, 3).cuda())
+
+
+def test_log_quantize_default_offset_is_the_reference_default():
+    """_model.quantize(log_model=True) with offset=None uses LOG_OFFSET_7_ADJUSTED, the default of
+    qmc/quantization_model_log.py:9."""
+    from quantized_spectrum_cartography_amd import utils
+    from quantized_spectrum_cartography_amd._model import quantize
+    g = torch.Generator().manual_seed(5)
+    X = torch.rand(4, 8, 8, generator=g)
+    n = torch.randn(X.shape, generator=g)
+    b = torch.tensor(utils.QUANTIZATION_BOUNDARIES_4_BINS_LOG if hasattr(utils, "QUANTIZATION_BOUNDARIES_4_BINS_LOG") else [-30.0, -12.0, -8.0, -4.0, 5.0])
+    a = quantize(X, 1.0, b, log_model=True, noise=n)
+    c = quantize(X, 1.0, b, offset=utils.LOG_OFFSET_7_ADJUSTED, log_model=True, noise=n)
+    assert torch.equal(a.cpu(), c.cpu())

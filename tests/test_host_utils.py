@@ -2,6 +2,7 @@
 reference's own outputs (tests/golden/nlls.npz from running qmc/nlls.py; the qmc/utils.py:43-51
 constants) and the oracle restatement."""
 import numpy as np
+import pytest
 import torch
 
 from oracle import nlls as onlls
@@ -35,3 +36,14 @@ def test_design_log_bins_equal_count():
     # the fitted log edges are close to equally spaced (the purpose of the fit)
     d = np.diff(edges[1:-1])
     assert np.all(d > 0)
+
+
+def test_log_quantize_rejects_nonpositive_offset():
+    """quantize(log_model=True) validates the offset before any device work."""
+    import torch
+    from quantized_spectrum_cartography_amd._model import quantize
+    X = torch.rand(2, 3, 3)
+    b = torch.tensor([-30.0, -2.0, 0.0, 2.0])
+    for off in (0.0, -1e-3):
+        with pytest.raises(ValueError):
+            quantize(X, 1.0, b, offset=off, log_model=True, noise=torch.zeros(X.shape))
