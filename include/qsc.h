@@ -354,6 +354,20 @@ QSC_API int qsc_state_flush(const qsc_obs_desc* d, int32_t R, qsc_state* st, flo
 QSC_API int qsc_supdate(const qsc_obs_desc* d, int32_t R, float* S, float* mS, float* vS,
                         const float* g, const qsc_adam* adam, float lambda_s, qsc_state* st,
                         void* ws, size_t ws_bytes, void* stream);
+/* K-slab S update of this rank's shard (reduce-scatter of the partial dS ->
+ * Adam on the owned 1/N of S -> all-gather): the slices [s0, s1) of S, mS, vS are updated from
+ * g_own, the shard's reduce-scattered gradient ((s1-s0)*QSC_SLICE rows of RP floats, slice s0
+ * first), exactly as qsc_supdate updates them; other slices are untouched.  Same state
+ * protocol (the per-slice ||S_new||^2 partials of the shard; see qsc_slice_nsq). */
+QSC_API int qsc_supdate_slices(const qsc_obs_desc* d, int32_t R, int32_t s0, int32_t s1,
+                               float* S, float* mS, float* vS, const float* g_own,
+                               const qsc_adam* adam, float lambda_s, qsc_state* st, void* ws,
+                               size_t ws_bytes, void* stream);
+/* per-slice ||S||^2 partials of every slice of S (into the pass workspace), bit-identical to
+ * those qsc_supdate / qsc_supdate_slices write for the same rows: run after the all-gather of
+ * the updated shards so the pending S-update settles the global ||S_new||^2 on every rank. */
+QSC_API int qsc_slice_nsq(const qsc_obs_desc* d, int32_t R, const float* S, void* ws,
+                          size_t ws_bytes, void* stream);
 /* ||x||^2 into *out (fp32, fixed order), e.g. the local ||C_slab||^2 before an all-reduce */
 QSC_API int qsc_sumsq_small(const float* x, int32_t n, float* out, void* stream);
 /* diagnostics: out[0..n) = ocml erff(x), out[n..2n) = the erf of the fused passes (erf_fast) */

@@ -109,10 +109,15 @@ def lib():
             except Exception as e:  # pragma: no cover - depends on toolchain
                 raise QscError("libqsc_hip.so is missing and could not be built: %s" % e)
         L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        missing = []
         for name, (res, args) in parse_header().items():
-            fn = getattr(L, name)
+            fn = getattr(L, name, None)
+            if fn is None:  # an older variant library (QSC_LIB_PATH): fails when called
+                missing.append(name)
+                continue
             fn.restype = res
             fn.argtypes = args
+        L.qsc_missing_ = missing
         _lib = L
     return _lib
 

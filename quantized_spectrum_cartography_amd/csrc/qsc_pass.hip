@@ -1950,6 +1950,64 @@ __global__ void __launch_bounds__(kSBlock) supdate_kernel(
   if (lane == 0) part_nsq[s] = nsq;
 }
 
+// K-slab S update on this rank's shard of slices [s0, s0 + gridDim slices) with the shard's
+// reduce-scattered gradient g_own (rows of slice s0 first): the same lane mapping, Adam and
+// per-slice ||S_new||^2 partial as supdate_kernel, for the owned rows only
+template <int RP>
+__global__ void __launch_bounds__(kSBlock) supdate_slices_kernel(
+    int s0, int s1, float* __restrict__ S, float* __restrict__ mS, float* __restrict__ vS,
+    const float* __restrict__ g_own, qsc_adam ad, float lambda_s, qsc_state* __restrict__ st,
+    float* __restrict__ part_nsq) {
+  constexpr int RH = RP / 2;
+  __shared__ Scalars sc;
+  if (threadIdx.x == 0) {
+    const float nrm = sqrtf(st->normsq_s);
+    sc.coef = nrm > 0.0f ? lambda_s / nrm : 0.0f;
+    sc.as = adam_scalars(ad, st->step_s + 1);
+    if (blockIdx.x == 0) st->pending |= QSC_PEND_SUPD;  // normsq_s / step_s settled later
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int s = s0 + blockIdx.x * kSWaves + wave;
+  if (s >= s1) return;
+  const int64_t lo = ((int64_t)(lane & (QSC_SLICE - 1))) * RP + (lane >> 5) * RH;
+  const int64_t o = (int64_t)s * QSC_SLICE * RP + lo;
+  const int64_t og = (int64_t)(s - s0) * QSC_SLICE * RP + lo;
+  float p[RH], m[RH], v[RH], g[RH];
+  ld_row<RH>(S + o, p);
+  ld_row<RH>(mS + o, m);
+  ld_row<RH>(vS + o, v);
+  ld_row<RH>(g_own + og, g);
+  float nsq = adam_row_fast<RH>(p, m, v, g, sc.coef, sc.as);
+  st_row<RH>(S + o, p);
+  st_row<RH>(mS + o, m);
+  st_row<RH>(vS + o, v);
+  nsq = wave_sum(nsq);
+  if (lane == 0) part_nsq[s] = nsq;
+}
+
+// Per-slice ||S||^2 partials of a replicated S, bit-identical to the ones supdate_kernel /
+// supdate_slices_kernel compute from the same rows (same lane mapping, the same fma chain over
+// the lane's half row, the same wave sum): after the K-slab all-gather every rank holds every
+// slice's partial without exchanging them
+template <int RP>
+__global__ void __launch_bounds__(kSBlock) slice_nsq_kernel(int nslices,
+                                                            const float* __restrict__ S,
+                                                            float* __restrict__ part_nsq) {
+  constexpr int RH = RP / 2;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int s = blockIdx.x * kSWaves + wave;
+  if (s >= nslices) return;
+  const int64_t o = ((int64_t)s * QSC_SLICE + (lane & (QSC_SLICE - 1))) * RP + (lane >> 5) * RH;
+  float p[RH];
+  ld_row<RH>(S + o, p);
+  float nsq = 0.0f;
+#pragma unroll
+  for (int j = 0; j < RH; ++j) nsq = __builtin_fmaf(p[j], p[j], nsq);
+  nsq = wave_sum(nsq);
+  if (lane == 0) part_nsq[s] = nsq;
+}
+
 __global__ void state_init_kernel(qsc_state* st, const double* nsq_part, int nparts) {
   if (threadIdx.x == 0) {
     double s = 0.0;
@@ -2403,6 +2461,49 @@ QSC_API int qsc_supdate(const qsc_obs_desc* d, int32_t R, float* S, float* mS, f
     hipLaunchKernelGGL(supdate_kernel<8>, grid, blk, 0, hs, nslices, S, mS, vS, g, *adam, lambda_s, st, w.snsq);
   else
     hipLaunchKernelGGL(supdate_kernel<16>, grid, blk, 0, hs, nslices, S, mS, vS, g, *adam, lambda_s, st, w.snsq);
+  QSC_CHECK_LAUNCH();
+  return QSC_OK;
+}
+
+QSC_API int qsc_supdate_slices(const qsc_obs_desc* d, int32_t R, int32_t s0, int32_t s1,
+                               float* S, float* mS, float* vS, const float* g_own,
+                               const qsc_adam* adam, float lambda_s, qsc_state* st, void* ws,
+                               size_t ws_bytes, void* stream) {
+  const int nslices = d ? d->Pp / QSC_SLICE : 0;
+  if (!desc_ok(d) || R < 1 || R > QSC_MAX_R || !S || !mS || !vS || !g_own || !adam || !st ||
+      !ws || ws_bytes < ws_bytes_for(d, R) || s0 < 0 || s1 < s0 || s1 > nslices)
+    return QSC_EINVAL;
+  PassWs w = carve(d, R, ws);
+  const int n = s1 - s0;
+  const dim3 grid((unsigned)std::max<int64_t>(1, ceil_div(n, kSWaves))), blk(kSBlock);
+  const int RP = rp_of(R);
+  hipStream_t hs = STREAM(stream);
+  // (an empty shard still launches one block: it raises the pending S-update flag like the rest)
+  if (RP == 4)
+    hipLaunchKernelGGL(supdate_slices_kernel<4>, grid, blk, 0, hs, s0, s1, S, mS, vS, g_own, *adam, lambda_s, st, w.snsq);
+  else if (RP == 8)
+    hipLaunchKernelGGL(supdate_slices_kernel<8>, grid, blk, 0, hs, s0, s1, S, mS, vS, g_own, *adam, lambda_s, st, w.snsq);
+  else
+    hipLaunchKernelGGL(supdate_slices_kernel<16>, grid, blk, 0, hs, s0, s1, S, mS, vS, g_own, *adam, lambda_s, st, w.snsq);
+  QSC_CHECK_LAUNCH();
+  return QSC_OK;
+}
+
+QSC_API int qsc_slice_nsq(const qsc_obs_desc* d, int32_t R, const float* S, void* ws,
+                          size_t ws_bytes, void* stream) {
+  if (!desc_ok(d) || R < 1 || R > QSC_MAX_R || !S || !ws || ws_bytes < ws_bytes_for(d, R))
+    return QSC_EINVAL;
+  PassWs w = carve(d, R, ws);
+  const int nslices = d->Pp / QSC_SLICE;
+  const dim3 grid((unsigned)ceil_div(nslices, kSWaves)), blk(kSBlock);
+  const int RP = rp_of(R);
+  hipStream_t hs = STREAM(stream);
+  if (RP == 4)
+    hipLaunchKernelGGL(slice_nsq_kernel<4>, grid, blk, 0, hs, nslices, S, w.snsq);
+  else if (RP == 8)
+    hipLaunchKernelGGL(slice_nsq_kernel<8>, grid, blk, 0, hs, nslices, S, w.snsq);
+  else
+    hipLaunchKernelGGL(slice_nsq_kernel<16>, grid, blk, 0, hs, nslices, S, w.snsq);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }

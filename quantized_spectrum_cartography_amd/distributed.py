@@ -10,14 +10,21 @@ Y[:, pixels] and its rows of S — and a replica of C (R x K, 8 KB at C3).  Per 
           uses the all-reduced ||S||^2 delivered by the C-step's collective.
 One small collective per iteration; S never crosses the fabric.
 
-K-slab (the north-star layout): rank g owns the frequency bins [k0, k1) — its slab of the
-observations Y[k0:k1] and of the spectra C[:, k0:k1] — and a replica of S.  Per outer iteration
+K-slab (the north-star layout): rank g owns the frequency bins [k0, k1) — its
+slab of the observations Y[k0:k1] and of the spectra C[:, k0:k1] — and a replica of S.  Per
+outer iteration
   C-step: local C-pass; the non-squared regulariser lambda_c ||C||_F needs the GLOBAL ||C||^2,
           so the ranks all-reduce one float before the fused cfinish (Adam + projection);
-  S-step: local S-pass in gradient mode (partial dS over the slab's bins), an all-reduce of
-          dS (Pp x RP fp32 — 8.4 MB at 512x512, R = 8), then the fused S update (regulariser,
-          Adam) on every rank; all ranks end with bit-identical S because the all-reduced dS is
-          identical everywhere.
+  S-step: local S-pass in gradient mode (partial dS over the slab's bins); a REDUCE-SCATTER of
+          dS (Pp x RP fp32, 8.4 MB at 512x512, R = 8) leaves rank g the summed gradient of its
+          1/N of the position slices; Adam on those rows only (qsc_supdate_slices: 1/N of the
+          S/mS/vS traffic); an ALL-GATHER of the updated shards (in place in S) re-replicates S;
+          every rank then recomputes the per-slice ||S_new||^2 partials from the gathered S
+          (qsc_slice_nsq, bit-identical to the ones the shard updates produced), so the
+          regulariser norm of the next step is the same on all ranks without another collective.
+          Same bytes on the fabric as one all-reduce, 1/N of the Adam traffic per rank.
+The next C-pass reads every tile's new S rows, which exist only after the all-gather, so the
+S update cannot be fused into it the way qsc_scpass fuses IJ-slab's.
 The pixel order of S (positions) is derived from the GLOBAL per-pixel observation counts
 (all-reduced once at setup) so that every rank lays S out identically.
 
@@ -168,12 +175,30 @@ class KSlabSolver:
             from .fused import PassEngine
             engine = PassEngine(obs, R, hist_cap=hist_cap)
         self.engine = engine
-        self.S = obs.to_positions(S_init.reshape(R, -1))
-        dev = self.S.device
+        S_pos = obs.to_positions(S_init.reshape(R, -1))
+        dev = S_pos.device
+        # shards of whole position slices (the engine's row unit): rank g owns rows
+        # [g*chunk, (g+1)*chunk) of S; S, dS are padded to N*chunk rows so that the
+        # reduce-scatter / all-gather move equal contiguous chunks (padding rows stay zero)
+        ws = dist.get_world_size()
+        self.rank = dist.get_rank() if ws > 1 else 0
+        unit = getattr(engine, "row_unit", 1)
+        Pp = S_pos.shape[0]
+        units = -(-Pp // unit)
+        self.chunk = -(-units // ws) * unit
+        self.r0 = min(self.rank * self.chunk, Pp)
+        self.r1 = min(self.r0 + self.chunk, Pp)
+        rows = ws * self.chunk
+        self.S_buf = torch.zeros((rows,) + tuple(S_pos.shape[1:]), dtype=torch.float32, device=dev)
+        self.S_buf[:Pp] = S_pos
+        self.S = self.S_buf[:Pp]
+        self.dS_buf = torch.zeros_like(self.S_buf)
+        self.dS = self.dS_buf[:Pp]
+        self.dS_own = torch.zeros((self.chunk,) + tuple(S_pos.shape[1:]), dtype=torch.float32,
+                                  device=dev)
         self.C = C_init_local.detach().to(dev, torch.float32).reshape(R, obs.K).clone()
         self.mS, self.vS = torch.zeros_like(self.S), torch.zeros_like(self.S)
         self.mC, self.vC = torch.zeros_like(self.C), torch.zeros_like(self.C)
-        self.dS = torch.empty_like(self.S)
         self.nsq_c = torch.zeros(1, dtype=torch.float32, device=dev)
         self.adam_c = _lib.make_adam(lr_c, betas, eps, project_nonneg=project_c)
         self.adam_s = _lib.make_adam(lr_s, betas, eps, project_nonneg=False)
@@ -196,8 +221,13 @@ class KSlabSolver:
     def s_step(self):
         e = self.engine
         e.spass(self.S, self.C, 0, dS=self.dS)
-        self.dist.all_reduce(self.dS)
-        e.supdate(self.S, self.mS, self.vS, self.dS, self.adam_s, self.lambda_s)
+        # reduce-scatter -> Adam on the owned rows -> all-gather (in place in S_buf)
+        self.dist.reduce_scatter_tensor(self.dS_own, self.dS_buf)
+        e.supdate_rows(self.S, self.mS, self.vS, self.dS_own, self.adam_s, self.lambda_s,
+                       self.r0, self.r1)
+        lo = self.rank * self.chunk
+        self.dist.all_gather_into_tensor(self.S_buf, self.S_buf[lo:lo + self.chunk])
+        e.slice_nsq(self.S)
 
     def iteration(self):
         self.c_step()

@@ -90,6 +90,24 @@ class PassEngine:
                   _lib.ptr(g), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),
                   self.ws.numel(), _lib.stream())
 
+    # K-slab shards: rows are dealt in whole position slices
+    row_unit = _lib.QSC_SLICE
+
+    def supdate_rows(self, S_pos, mS, vS, g_own, adam, lambda_s, r0, r1):
+        """Adam on position rows [r0, r1) (multiples of QSC_SLICE) from the shard's gradient
+        g_own (its first row is row r0) -- qsc_supdate_slices."""
+        u = _lib.QSC_SLICE
+        if r0 % u or (r1 % u and r1 != self.obs.Pp):
+            raise ValueError("shard rows must be whole position slices")
+        _lib.call("qsc_supdate_slices", self.desc, self.R, r0 // u, -(-r1 // u), _lib.ptr(S_pos),
+                  _lib.ptr(mS), _lib.ptr(vS), _lib.ptr(g_own), adam, float(lambda_s),
+                  _lib.ptr(self.state), _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
+
+    def slice_nsq(self, S_pos):
+        """Every slice's ||S||^2 partial from the (all-gathered) S -- qsc_slice_nsq."""
+        _lib.call("qsc_slice_nsq", self.desc, self.R, _lib.ptr(S_pos), _lib.ptr(self.ws),
+                  self.ws.numel(), _lib.stream())
+
     def cupdate(self, C, mC, vC, g, adam, lambda_c, normsq_s_ext=None):
         """C update from an all-reduced gradient g (R*K [+1]) (IJ-slab sharding)."""
         _lib.call("qsc_cupdate", self.R, self.obs.K, _lib.ptr(C), _lib.ptr(mC), _lib.ptr(vC),

@@ -3,8 +3,8 @@
 The solver is written against a small engine interface (fused.PassEngine on the GPU).  Here it
 runs over a CPU emulation of that interface whose gradients come from the oracle's closed-form
 math (oracle/explicit.py, fp64), so the test checks the sharding itself: the per-slab C-passes,
-the all-reduced ||C||^2 of the non-squared regulariser, the all-reduce of the partial S-gradient
-and the replicated S update.  Two ranks, each holding half of the frequency bins, must reproduce
+the all-reduced ||C||^2 of the non-squared regulariser, and the reduce-scatter of the partial
+S-gradient, the Adam update of each rank's shard of S and the all-gather that re-replicates it.  Two ranks, each holding half of the frequency bins, must reproduce
 a single-process run over all bins, and both must follow the reference op sequence
 (oracle/solver.py) within the parity tolerance.
 """
@@ -38,10 +38,11 @@ class _Obs:
         self.Wx = Wx.reshape(self.K, -1).numpy()
 
     def to_positions(self, X):
-        return X.detach().reshape(X.shape[0], self.P).to(torch.float32).clone()
+        """(R, P) -> position order (Pp, R): position-major rows, as the device layout"""
+        return X.detach().reshape(X.shape[0], self.P).to(torch.float32).t().contiguous()
 
     def to_pixels(self, Xp, R):
-        return Xp.clone()
+        return Xp.t().contiguous()
 
 
 class _CpuEngine:
@@ -56,8 +57,10 @@ class _CpuEngine:
         self.calls = []
 
     def _grad(self, S, C):
-        return explicit.nll_grad(S.double().numpy(), C.double().numpy(), self.obs.Y, self.obs.Wx,
-                                 self.b, self.sigma)
+        """fp64 NLL, dS (position order, like S), dC"""
+        nll, gS, gC = explicit.nll_grad(S.t().double().numpy(), C.double().numpy(), self.obs.Y,
+                                        self.obs.Wx, self.b, self.sigma)
+        return nll, np.ascontiguousarray(gS.T), gC
 
     @staticmethod
     def _adam(p, m, v, g, step, adam):
@@ -122,6 +125,20 @@ class _CpuEngine:
         self.spass(S, C, 1, mS=mS, vS=vS, adam=adam, lambda_s=lambda_s)
         self.cpass(S, C)
 
+    row_unit = 1
+
+    def supdate_rows(self, S, mS, vS, g_own, adam, lambda_s, r0, r1):
+        """qsc_supdate_slices: Adam on rows [r0, r1) from the shard's reduce-scattered gradient"""
+        nrm = math.sqrt(self.st["normsq_s"])
+        gg = g_own[: r1 - r0] + (lambda_s / nrm if nrm > 0 else 0.0) * S[r0:r1]
+        self.st["step_s"] += 1
+        self._adam(S[r0:r1], mS[r0:r1], vS[r0:r1], gg, self.st["step_s"], adam)
+        self.calls.append("supdate_rows")
+
+    def slice_nsq(self, S):
+        """qsc_slice_nsq: ||S||^2 of the all-gathered S (every rank the same)"""
+        self.st["normsq_s"] = float((S.double() ** 2).sum())
+
     def supdate(self, S, mS, vS, g, adam, lambda_s):
         nrm = math.sqrt(self.st["normsq_s"])
         gg = g + (lambda_s / nrm if nrm > 0 else 0.0) * S
@@ -166,6 +183,14 @@ class _SoloDist:
     def all_gather(outs, t):
         outs[0].copy_(t)
 
+    @staticmethod
+    def reduce_scatter_tensor(out, t):
+        out.copy_(t)
+
+    @staticmethod
+    def all_gather_into_tensor(out, t):
+        out.copy_(t)
+
 
 def _run(dist_mod, rank, world):
     from quantized_spectrum_cartography_amd.distributed import KSlabSolver, kslab_bounds
@@ -175,7 +200,12 @@ def _run(dist_mod, rank, world):
     eng = _CpuEngine(obs, b.numpy(), sigma)
     sol = KSlabSolver(obs, S0, C0[:, k0:k1], dist=dist_mod, engine=eng)
     sol.run(ITERS)
-    return sol.S_pixels().reshape(R, I * J), sol.C_global(), eng.read_state()
+    # reduce-scatter -> Adam on the owned 1/N of S -> all-gather
+    assert eng.calls.count("supdate_rows") == ITERS
+    assert sol.r1 - sol.r0 <= -(-I * J // world)
+    st = eng.read_state()
+    st["shard"] = (sol.r0, sol.r1)
+    return sol.S_pixels().reshape(R, I * J), sol.C_global(), st
 
 
 def _run_ij(dist_mod, rank, world):
@@ -195,7 +225,8 @@ def _worker(rank, world, port, out_path, mode):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         S, C, st = (_run if mode == "k" else _run_ij)(dist, rank, world)
-        np.savez(out_path + ".r%d" % rank, S=S.numpy(), C=C.numpy(), step_s=st["step_s"])
+        np.savez(out_path + ".r%d" % rank, S=S.numpy(), C=C.numpy(), step_s=st["step_s"],
+                 shard=np.array(st.get("shard", (0, 0))))
     finally:
         dist.destroy_process_group()
 
@@ -225,9 +256,12 @@ def test_kslab_two_ranks_match_single_process(tmp_path):
     two = np.load(out + ".r0.npz")
     r1 = np.load(out + ".r1.npz")
     S1, C1, _ = _run(_SoloDist, 0, 1)
-    # S is replicated: both ranks hold the same (all-reduced gradient, same update)
+    # S is replicated: both ranks hold the same S after the all-gather of the updated shards
     assert np.array_equal(two["S"], r1["S"])
     assert int(two["step_s"]) == ITERS
+    # the two shards are disjoint and cover every position row
+    (a0, a1), (b0, b1) = two["shard"], r1["shard"]
+    assert a0 == 0 and a1 == b0 and b1 == I * J
     # sharded == single process up to the summation order of the partial S-gradients
     assert rel_fro(two["S"], S1.numpy()) < 1e-6
     assert rel_fro(two["C"], C1.numpy()) < 1e-6
