@@ -370,6 +370,11 @@ QSC_API int qsc_slice_nsq(const qsc_obs_desc* d, int32_t R, const float* S, void
                           size_t ws_bytes, void* stream);
 /* ||x||^2 into *out (fp32, fixed order), e.g. the local ||C_slab||^2 before an all-reduce */
 QSC_API int qsc_sumsq_small(const float* x, int32_t n, float* out, void* stream);
+/* debug builds (QSC_DEBUG=1, _build.py --debug): the source line of the last failed bounds
+ * check in the pass kernels (entry offsets, gather-table rows, lane bins; a failed check is
+ * recorded and its index clamped, never trapped), 0 if none, -1 in release builds.
+ * SYNCHRONOUS (device synchronise); clear != 0 resets the flag. */
+QSC_API int qsc_debug_status(int32_t clear);
 /* diagnostics: out[0..n) = ocml erff(x), out[n..2n) = the erf of the fused passes (erf_fast) */
 QSC_API int qsc_selftest_erf(const float* x, int32_t n, float* out, void* stream);
 

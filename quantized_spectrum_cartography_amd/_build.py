@@ -46,7 +46,7 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force=False, verbose=True, out=None, extra_flags=()):
+def build(force=False, verbose=True, out=None, extra_flags=(), link_flags=()):
     """Compile every HIP source for gfx950 and link libqsc_hip.so (parallel, one hipcc per file).
 
     `out` / `extra_flags` produce a variant library (e.g. -DQSC_SPASS_WAVES=4 for tuning runs,
@@ -77,7 +77,8 @@ def build(force=False, verbose=True, out=None, extra_flags=()):
             msg = "\n".join("---- %s ----\n%s" % f for f in failed)
             raise RuntimeError("hipcc failed:\n" + msg)
         out_tmp = lib_path + ".tmp"
-        cmd = [hipcc, "-shared", "-fPIC", "--offload-arch=" + ARCH] + objs + ["-o", out_tmp]
+        cmd = ([hipcc, "-shared", "-fPIC", "--offload-arch=" + ARCH] + list(link_flags) + objs +
+               ["-o", out_tmp])
         subprocess.check_call(cmd)
         os.replace(out_tmp, lib_path)
     finally:
@@ -87,5 +88,31 @@ def build(force=False, verbose=True, out=None, extra_flags=()):
     return lib_path
 
 
+# Debug variants: QSC_DEBUG=1 bounds checks in the pass kernels
+# (qsc_common.cuh QSC_DCHECK, read back with qsc_debug_status); "asan" adds AddressSanitizer to
+# the HOST code of the C ABI (argument checks, workspace carving, the host scheduler), loaded
+# with the clang ASan runtime preloaded (tools/asan_check.sh).  Device code is never sanitized.
+DEBUG_FLAGS = ["-DQSC_DEBUG=1", "-g"]
+ASAN_FLAGS = DEBUG_FLAGS + ["-Xarch_host", "-fsanitize=address", "-fno-omit-frame-pointer"]
+DEBUG_LIB = os.path.join(PKG_DIR, "libqsc_hip_debug.so")
+ASAN_LIB = os.path.join(PKG_DIR, "libqsc_hip_asan.so")
+
+
+def build_variant(kind):
+    """kind "debug" -> libqsc_hip_debug.so, "asan" -> libqsc_hip_asan.so (next to the release
+    library; select one with QSC_LIB_PATH)."""
+    if kind == "debug":
+        return build(out=DEBUG_LIB, extra_flags=DEBUG_FLAGS, verbose=False)
+    if kind == "asan":
+        return build(out=ASAN_LIB, extra_flags=ASAN_FLAGS, verbose=False,
+                     link_flags=["-Xarch_host", "-fsanitize=address", "-shared-libsan"])
+    raise ValueError(kind)
+
+
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--debug" in sys.argv:
+        print("built", build_variant("debug"))
+    elif "--asan" in sys.argv:
+        print("built", build_variant("asan"))
+    else:
+        build(force="--force" in sys.argv)

@@ -127,11 +127,21 @@ def err(code):
     return s.decode() if s else "error %d" % code
 
 
+# QSC_DEBUG_CHECK=1 (with a QSC_DEBUG=1 library, _build.py --debug): after every call outside
+# graph capture, synchronise and raise if a kernel bounds check failed (qsc_debug_status)
+_DEBUG_CHECK = os.environ.get("QSC_DEBUG_CHECK", "0") == "1"
+
+
 def call(name, *args):
     """Call a qsc_* entry point and raise QscError on a non-zero status."""
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         raise QscError("%s failed: %s (code %d)" % (name, err(rc), rc))
+    if _DEBUG_CHECK and not torch.cuda.is_current_stream_capturing():
+        line = lib().qsc_debug_status(1)
+        if line > 0:
+            raise QscError("%s: kernel bounds check failed at qsc_pass.hip:%d (QSC_DEBUG)"
+                           % (name, line))
     return rc
 
 

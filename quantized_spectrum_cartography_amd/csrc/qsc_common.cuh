@@ -193,7 +193,30 @@ struct Lik {
   float ob_scale; // fp32(sqrt(log2 e) / a): the factor rows are pre-scaled by -ob_scale
   float ob_thr;   // fp32(thr * sqrt(log2 e) / a)
   float ob_kg;    // fp32(kgrad / kMillsK)
+  // bounds the QSC_DEBUG build checks (set by the launchers; unused otherwise): rows of the
+  // C^T gather table [0] and of the S-tile table [1], entries of the S / C formats
+  int dbg_rows[2];
+  int64_t dbg_ent[2];
 };
+
+// QSC_DEBUG=1 builds (_build.py --debug): bounds checks in the pass kernels.  A failed check
+// never traps (a GPU exception can take the whole node down): it records the line in a device
+// flag, the offending index is clamped into range so the kernel finishes, and the host reads
+// the flag with qsc_debug_status after the call.
+#ifndef QSC_DEBUG
+#define QSC_DEBUG 0
+#endif
+#if QSC_DEBUG
+extern __device__ int g_qsc_dbg_line;
+#define QSC_DCHECK(c)                                      \
+  do {                                                     \
+    if (!(c)) atomicMax(&::qsc::g_qsc_dbg_line, __LINE__); \
+  } while (0)
+#else
+#define QSC_DCHECK(c) \
+  do {                \
+  } while (0)
+#endif
 
 // one-bit Mills-ratio form.  With c = sqrt(log2 e) and u = c |z|, the probit tail
 // 0.5 erfc(|z|) = exp(-z^2) * 0.5 erfcx(|z|) is evaluated as
@@ -228,6 +251,8 @@ inline Lik make_lik(const qsc_model* m) {
   l.ob_scale = (float)(c / (double)l.a);
   l.ob_thr = (float)((double)l.thr * c / (double)l.a);
   l.ob_kg = (float)((double)p.kgrad / kMillsK);
+  l.dbg_rows[0] = l.dbg_rows[1] = 0;
+  l.dbg_ent[0] = l.dbg_ent[1] = 0;
 #if QSC_FTZ_SAT
   l.ob_kg = (float)((double)p.kgrad / kMillsK * 0x1p101);  // E is carried 2^-101 low
 #endif

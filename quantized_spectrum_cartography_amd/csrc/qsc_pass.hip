@@ -24,6 +24,12 @@
 
 using namespace qsc;
 
+#if QSC_DEBUG
+namespace qsc {
+__device__ int g_qsc_dbg_line = 0;  // the QSC_DCHECK flag (qsc_common.cuh)
+}
+#endif
+
 namespace {
 
 constexpr int kSBlock = 256;   // S-pass / S-update: 4 waves = 4 slices of QSC_SLICE pixels
@@ -266,13 +272,23 @@ struct Scalars {
 #ifndef QSC_DIAG_NOCONF_S
 #define QSC_DIAG_NOCONF_S 0
 #endif
-template <int RP, typename E, int KIND, int DG = 0>
+// TBL: the table gathered from, 0 = C^T (S-step), 1 = the S tile (C-pass)
+template <int RP, typename E, int KIND, int TBL = 0>
 __device__ __forceinline__ void pair_rows(uint32_t ea, uint32_t eb, const f2v (&own)[RP / 2],
                                           const float* __restrict__ tab, f2v (&oa)[RP / 2],
                                           f2v (&ob)[RP / 2], f2v& tha, f2v& thb, const Lik& lk) {
   using T = Ent<E>;
   constexpr int P = TP<RP, KIND>::v;
+  constexpr int DG = TBL == 1 ? QSC_DIAG_NOCONF_C : QSC_DIAG_NOCONF_S;
   uint32_t ia = is_sr(KIND) ? ea : (ea & T::kMask), ib = is_sr(KIND) ? eb : (eb & T::kMask);
+#if QSC_DEBUG
+  {
+    const uint32_t lim = (uint32_t)lk.dbg_rows[TBL];
+    QSC_DCHECK(ia < lim && ib < lim);
+    ia = ia < lim ? ia : 0u;
+    ib = ib < lim ? ib : 0u;
+  }
+#endif
   if constexpr (DG != 0) {
     // diagnostic builds only (wrong values): every 16-lane group of a ds_read_b128 reads rows of
     // 16 distinct residues mod 16, i.e. conflict-free gathers (bounds the bank-conflict cost)
@@ -313,14 +329,14 @@ __device__ __forceinline__ void pair_math(uint32_t ea, uint32_t eb, const f2v (&
                                           const float2* __restrict__ edges, const Lik& lk,
                                           f2v (&acc)[RP / 2], f2v& nll, f2v& pq, bool valid);
 
-template <int RP, typename E, int KIND, bool LOG>
+template <int RP, typename E, int KIND, bool LOG, int TBL>
 __device__ __forceinline__ void pair_step(uint32_t ea, uint32_t eb, const f2v (&own)[RP / 2],
                                           const float* __restrict__ tab,
                                           const float2* __restrict__ edges, const Lik& lk,
                                           f2v (&acc)[RP / 2], f2v& nll, bool valid) {
   f2v oa[RP / 2], ob[RP / 2];
   f2v tha, thb, pq;
-  pair_rows<RP, E, KIND>(ea, eb, own, tab, oa, ob, tha, thb, lk);
+  pair_rows<RP, E, KIND, TBL>(ea, eb, own, tab, oa, ob, tha, thb, lk);
   pair_math<RP, E, KIND, LOG>(ea, eb, own, oa, ob, tha, thb, edges, lk, acc, nll, pq, valid);
   if constexpr (is_sr(KIND)) nll -= log2_2(pq);  // (single pair: the walks pair them up)
 }
@@ -395,8 +411,8 @@ __device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const f2v (&
                                       f2v (&acc)[RP / 2], f2v& nll, bool valid = true) {
   uint32_t e[4];
   Ent<E>::unpack(v, e);
-  pair_step<RP, E, KIND, LOG>(e[0], e[1], own, tab, edges, lk, acc, nll, valid);
-  pair_step<RP, E, KIND, LOG>(e[2], e[3], own, tab, edges, lk, acc, nll, valid);
+  pair_step<RP, E, KIND, LOG, 1>(e[0], e[1], own, tab, edges, lk, acc, nll, valid);
+  pair_step<RP, E, KIND, LOG, 1>(e[2], e[3], own, tab, edges, lk, acc, nll, valid);
 }
 
 // half a chunk (the S-pass lane's unit: the pixel's two lanes split every chunk)
@@ -407,7 +423,7 @@ __device__ __forceinline__ void half_chunk(const typename Ent<E>::V2& v, const f
                                            f2v (&acc)[RP / 2], f2v& nll) {
   uint32_t e[2];
   Ent<E>::unpack2(v, e);
-  pair_step<RP, E, KIND, LOG>(e[0], e[1], own, tab, edges, lk, acc, nll, true);
+  pair_step<RP, E, KIND, LOG, 0>(e[0], e[1], own, tab, edges, lk, acc, nll, true);
 }
 
 // Read-ahead of a lane list in groups of NB chunks (chunk j at src[j * row], row in V4 units).
@@ -449,7 +465,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
   {
     uint32_t e[4];
     Ent<E>::unpack(b[0], e);
-    pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_C>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
+    pair_rows<RP, E, KIND, 1>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
   }
 #endif
   for (;;) {
@@ -465,13 +481,13 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
         Ent<E>::unpack(b[i], e);
         f2v xa[RP / 2], xb[RP / 2];
         f2v txa, txb, pqa, pqb;
-        pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_C>(e[2], e[3], own, tab, xa, xb, txa, txb, lk);
+        pair_rows<RP, E, KIND, 1>(e[2], e[3], own, tab, xa, xb, txa, txb, lk);
         pair_math<RP, E, KIND, LOG>(e[0], e[1], own, ra, rb, tra, trb, edges, lk, acc, nll, pqa,
                                     true);
         if (i + 1 < kGroup) {
           uint32_t f[4];
           Ent<E>::unpack(b[i + 1], f);
-          pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_C>(f[0], f[1], own, tab, ra, rb, tra, trb, lk);
+          pair_rows<RP, E, KIND, 1>(f[0], f[1], own, tab, ra, rb, tra, trb, lk);
         }
         pair_math<RP, E, KIND, LOG>(e[2], e[3], own, xa, xb, txa, txb, edges, lk, acc, nll, pqb,
                                     true);
@@ -486,7 +502,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
     {
       uint32_t e[4];
       Ent<E>::unpack(b[0], e);
-      pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_C>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
+      pair_rows<RP, E, KIND, 1>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
     }
 #else
 #pragma unroll
@@ -527,7 +543,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
     {
       uint32_t e[2];
       Ent<E>::unpack2(b[0], e);
-      pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_S>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
+      pair_rows<RP, E, KIND, 0>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
     }
     for (;;) {
       const int jn = jb + kGroupS;
@@ -543,13 +559,13 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
           Ent<E>::unpack2(b[i], e);
           Ent<E>::unpack2(b[i + 1], f);
           f2v xa[RP / 2], xb[RP / 2], txa, txb, pa, pb = splat2(1.0f);
-          pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_S>(f[0], f[1], own, tab, xa, xb, txa, txb, lk);
+          pair_rows<RP, E, KIND, 0>(f[0], f[1], own, tab, xa, xb, txa, txb, lk);
           pair_math<RP, E, KIND, LOG>(e[0], e[1], own, ra, rb, tra, trb, edges, lk, acc, nll, pa,
                                       true);
           if (i + 2 < kGroupS) {
             uint32_t g[2];
             Ent<E>::unpack2(b[i + 2], g);
-            pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_S>(g[0], g[1], own, tab, ra, rb, tra, trb, lk);
+            pair_rows<RP, E, KIND, 0>(g[0], g[1], own, tab, ra, rb, tra, trb, lk);
           }
           if (jb + i + 1 < j1)
             pair_math<RP, E, KIND, LOG>(f[0], f[1], own, xa, xb, txa, txb, edges, lk, acc, nll,
@@ -563,7 +579,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
       {
         uint32_t e[2];
         Ent<E>::unpack2(b[0], e);
-        pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_S>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
+        pair_rows<RP, E, KIND, 0>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
       }
       jb = jn;
     }
@@ -585,7 +601,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
             uint32_t e[2];
             Ent<E>::unpack2(b[i], e);
             f2v oa[RP / 2], ob[RP / 2], tha, thb;
-            pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_S>(e[0], e[1], own, tab, oa, ob, tha, thb, lk);
+            pair_rows<RP, E, KIND, 0>(e[0], e[1], own, tab, oa, ob, tha, thb, lk);
             pair_math<RP, E, KIND, LOG>(e[0], e[1], own, oa, ob, tha, thb, edges, lk, acc, nll,
                                         pa, true);
           }
@@ -593,7 +609,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
             uint32_t e[2];
             Ent<E>::unpack2(b[i + 1], e);
             f2v oa[RP / 2], ob[RP / 2], tha, thb;
-            pair_rows<RP, E, KIND, QSC_DIAG_NOCONF_S>(e[0], e[1], own, tab, oa, ob, tha, thb, lk);
+            pair_rows<RP, E, KIND, 0>(e[0], e[1], own, tab, oa, ob, tha, thb, lk);
             pair_math<RP, E, KIND, LOG>(e[0], e[1], own, oa, ob, tha, thb, edges, lk, acc, nll,
                                         pb, true);
           }
@@ -971,6 +987,7 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     const bool more = s1 < nslices;  // wave-uniform
     // 3. next slice's reads (unconditional: a last slice re-reads itself, cache-resident, so
     //    the wait counts stay static)
+    QSC_DCHECK(s < nslices && off[s] + (int64_t)width[s] * QSC_SLICE <= lk.dbg_ent[0]);
     slice_load(q, ent, width, off, more ? s1 : s, ln, S, mS, vS);
     STAMP(w, 2 + 3 * i);
     const int64_t blk = (int64_t)s * QSC_SLICE * RP;  // the slice's rows (uniform)
@@ -1221,8 +1238,10 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
     j0 = (W4 * part) / NP;
     j1 = (W4 * (part + 1)) / NP;
     src = reinterpret_cast<const V4*>(ent + off[wi]);
+    QSC_DCHECK(off[wi] + (int64_t)width[wi] * 64 <= lk.dbg_ent[1]);
     load_group(src, lo, 64, j0, 1, max(j1 - 1, 0), buf);
     k = kmap[wi * 64 + lane];  // this lane's bin (count-sorted order)
+    QSC_DCHECK(k >= 0 && k < Kp);
 #pragma unroll
     for (int r = 0; r < RP; ++r) cv[r] = C[(int64_t)min(r, R - 1) * K + min(k, K - 1)];
   };
@@ -1544,6 +1563,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
       STAMP(wg, 12);
     }
 #endif
+    QSC_DCHECK(s < nt * nsl && s_off[s] + (int64_t)s_width[s] * QSC_SLICE <= lk.dbg_ent[0]);
     slice_load(q, s_ent, s_width, s_off, more ? global_of(il1) : s, ln, S, mS, vS);
     float sv[RP];
 #pragma unroll
@@ -1619,8 +1639,10 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
     j0 = (W4 * part) / NP;
     j1 = (W4 * (part + 1)) / NP;
     src = reinterpret_cast<const V4*>(c_ent + c_off[wi]);
+    QSC_DCHECK(c_off[wi] + (int64_t)c_width[wi] * 64 <= lk.dbg_ent[1]);
     load_group(src, lo, 64, j0, 1, max(j1 - 1, 0), buf);
     k = c_kmap[wi * 64 + lane];  // this lane's bin (count-sorted order)
+    QSC_DCHECK(k >= 0 && k < Kp);
 #pragma unroll
     for (int r = 0; r < RP; ++r) cv[r] = Cl[min(k, K - 1) * CP + r];  // C_i, as the S-step used
   };
@@ -2103,6 +2125,14 @@ void scale_edges(Edges* E, int nbins, float a) {
     E->e[c] = make_float2((float)((double)E->e[c].x / a), (float)((double)E->e[c].y / a));
 }
 
+// the QSC_DEBUG bounds of a launch (Lik::dbg_*): gather-table rows and entry counts
+void set_dbg(Lik& lk, const qsc_obs_desc* d, bool sr) {
+  lk.dbg_rows[0] = sr ? sr_rows(d->K) : d->K;
+  lk.dbg_rows[1] = sr ? sr_rows(d->PT) : d->PT;
+  lk.dbg_ent[0] = d->s_entries;
+  lk.dbg_ent[1] = d->c_entries;
+}
+
 // compute units of the current device (cached per device id)
 int cu_count() {
   static int cached[64] = {0};
@@ -2212,7 +2242,8 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
   PassWs w = carve(d, R, ws);
   Edges E;
   make_edges(m, &E);
-  const Lik lk = make_lik(m);
+  Lik lk = make_lik(m);
+  set_dbg(lk, d, sr);
   if (kind == LIK_SQUARED)
     make_sq_targets(m, &E);
   else if (!m->log_model)
@@ -2257,7 +2288,8 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
   PassWs w = carve(d, R, ws);
   Edges E;
   make_edges(m, &E);
-  const Lik lk = make_lik(m);
+  Lik lk = make_lik(m);
+  set_dbg(lk, d, sr);
   if (kind == LIK_SQUARED)
     make_sq_targets(m, &E);
   else if (!m->log_model)
@@ -2377,7 +2409,8 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
   PassWs w = carve(d, R, ws);
   Edges E;
   make_edges(m, &E);
-  const Lik lk = make_lik(m);
+  Lik lk = make_lik(m);
+  set_dbg(lk, d, sr);
   if (kind == LIK_SQUARED)
     make_sq_targets(m, &E);
   else if (!m->log_model)
@@ -2521,6 +2554,22 @@ QSC_API int qsc_diag_stamps(unsigned long long* host, int n) {
                                   sizeof(unsigned long long) * (size_t)std::min(n, kStampWaves * kStamps));
 }
 #endif
+
+QSC_API int qsc_debug_status(int32_t clear) {
+#if QSC_DEBUG
+  int line = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(&line, HIP_SYMBOL(g_qsc_dbg_line), sizeof(int)) != hipSuccess) return -2;
+  if (clear && line) {
+    const int zero = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_qsc_dbg_line), &zero, sizeof(int)) != hipSuccess) return -2;
+  }
+  return line;
+#else
+  (void)clear;
+  return -1;
+#endif
+}
 
 QSC_API int qsc_selftest_erf(const float* x, int32_t n, float* out, void* stream) {
   if (n < 0 || !x || !out) return QSC_EINVAL;

@@ -140,6 +140,49 @@ def test_c5_dip_fused_dS_isolated():
     assert rel_fro(_np(S.grad, (R, P)), rdS) < TOL
 
 
+def test_gan_fused_dS_isolated(golden):
+    """The HIP part of the GAN path (qmc/qmc.ipynb :622-634, S = Generator256(Z),
+    deep_prior/networks/gan.py:83-126) isolated at the north_star tolerance: the fused S-pass
+    dS (and C-pass dC, NLL) at S = G(Z) on the generator's 51x51 output, with the notebook's
+    log model, 4 log bins, sigma = 5, offset LOG_OFFSET_4 and f = 0.1 on the shipped map
+    (onebitdata1.mat, tests/golden/mat_c1.npz), vs the fp64 oracle at 1e-5.  (Only the torch
+    generator's own backward, MIOpen vs CPU conv numerics, is held to 1e-4 end to end in
+    tests/test_gpu_fused.py::test_generator_solver_vs_oracle.)"""
+    from quantized_spectrum_cartography_amd import fused, nets
+    from quantized_spectrum_cartography_amd import quantization_model_log as qml
+    from quantized_spectrum_cartography_amd.obs import Observations
+    from quantized_spectrum_cartography_amd.utils import (LOG_OFFSET_4,
+                                                          QUANTIZATION_BOUNDARIES_4_BINS_LOG)
+    m = golden("mat_c1")
+    T = torch.from_numpy(m["T_true"].astype(np.float32))  # (64, 51, 51)
+    K, I, J = T.shape
+    R, P = 2, I * J
+    g = torch.Generator().manual_seed(31)
+    b = torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG)
+    Y = qml.quantize(T, 5.0, b, offset=LOG_OFFSET_4, noise=torch.randn(T.shape, generator=g))
+    Y = Y.cpu().unsqueeze(1)
+    Wx = torch.bernoulli(torch.full((K, 1, I, J), 0.1), generator=g)
+    assert len(torch.unique(Y)) >= 3
+    torch.manual_seed(3)
+    gen = nets.Generator256().cuda().eval()
+    Z = torch.randn((R, 256), generator=torch.Generator().manual_seed(4)).cuda()
+    with torch.no_grad():
+        S_gen = gen(Z).reshape(R, 1, I, J)
+    C0 = torch.from_numpy(m["C_true"].astype(np.float32)) * (0.5 + torch.rand(R, K, generator=g))
+    obs = Observations(Y, Wx, b, 5.0, offset=LOG_OFFSET_4, log_model=True, R_hint=R)
+    S = S_gen.clone().requires_grad_(True)
+    C = C0.cuda().requires_grad_(True)
+    nll = fused.ProbitNLL.apply(S, C, obs)
+    nll.backward()
+    ob = explicit.observed(_np(Y, (K, P)), _np(Wx, (K, P)))
+    rn, rdS, rdC = explicit.nll_grad_obs(_np(S_gen, (R, P)), _np(C0), ob, _np(b), 5.0,
+                                         LOG_OFFSET_4, True)
+    assert np.isfinite(rn)
+    assert abs(nll.item() - rn) / abs(rn) < TOL
+    assert rel_fro(_np(S.grad, (R, P)), rdS) < TOL
+    assert rel_fro(_np(C.grad), rdC) < TOL
+
+
 def test_c5_dip_solve_defaults_finite():
     """dip.solve with its defaults (offset = the reference log model's LOG_OFFSET, zero C
     init): the first C-pass sees T_hat = 0 and must stay finite."""
