@@ -2347,7 +2347,9 @@ static int cpass_parts(const qsc_obs_desc* d) {
 static bool scpass_fits(const qsc_obs_desc* d, int R, bool sr) {
   const int NP = cpass_parts(d);
   const int U = d->nks * NP;
-  return U >= 4 && U <= QSC_CTILE_MAXW && d->PT <= 4096 &&
+  // any unit count: small problems (C2: one 64-bin slice, ~13 entries per bin and tile, so one
+  // unit per tile) run their C-pass units on the first waves while the rest wait at the end
+  return U >= 1 && U <= QSC_CTILE_MAXW && d->PT <= 4096 &&
          scfused_lds(d->PT, R, d->K, d->nks, NP, sr) <= 160 * 1024;
 }
 

@@ -79,7 +79,7 @@ def _solver_check(prob, dims, ob, iters=3, log_model=False, offset=0.0, expect_f
     assert np.allclose(res.costs_c, cc, rtol=TOL) and np.allclose(res.costs_s, cs, rtol=TOL)
 
 
-@pytest.mark.parametrize("cfg,seed,fused", [("c2", 20262, False), ("c3", 20263, True)])
+@pytest.mark.parametrize("cfg,seed,fused", [("c2", 20262, True), ("c3", 20263, True)])
 def test_onebit_config_pass_and_solver(cfg, seed, fused):
     """C2 / C3 (BASELINE.md section 3 recipe, the bench's own inputs for C3)."""
     prob, dims = _onebit(cfg, seed)

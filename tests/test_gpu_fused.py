@@ -139,8 +139,8 @@ def test_solver_graph_replay_matches_eager():
     assert np.array_equal(a.C.cpu().numpy(), b.C.cpu().numpy())
 
 
-# tiles chosen so that every case has >= 4 C-pass units per tile (qsc_scpass_supported), i.e.
-# the fused launch really runs (asserted through SolveResult.fused)
+# the fused launch applies at every shape here, including one C-pass unit per tile (C2 class);
+# that it really runs is asserted through SolveResult.fused
 @pytest.mark.parametrize("seed,R,I,J,K,log_model,loss,nbins,tile",
                          [(41, 4, 64, 64, 64, False, "probit", 2, 512),
                           (42, 8, 96, 80, 256, False, "probit", 2, None),
@@ -152,7 +152,10 @@ def test_solver_graph_replay_matches_eager():
                           # rank 16 (8-wave launch, 20-float LDS pitch), R = 12 padded to 16
                           (49, 16, 64, 64, 256, False, "probit", 2, 512),
                           (50, 12, 48, 64, 192, False, "squared", 2, 256),
-                          (51, 16, 64, 64, 128, True, "probit", 2, 512)])
+                          (51, 16, 64, 64, 128, True, "probit", 2, 512),
+                          # one C-pass unit per tile (C2 shape class: K = 64, 128-position tiles)
+                          (52, 4, 64, 64, 64, False, "probit", 2, 128),
+                          (53, 4, 96, 64, 64, False, "probit", 2, None)])
 def test_fused_spass_cpass_bitexact(seed, R, I, J, K, log_model, loss, nbins, tile):
     """qsc_scpass (S-step + next C-pass in one launch) reproduces spass + cpass bit for bit:
     S, C and the cost history after n iterations, eager and hipGraph."""

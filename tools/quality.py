@@ -38,6 +38,10 @@ def main():
     ap.add_argument("--c2-iters", type=int, default=4000)
     ap.add_argument("--dip-iters", type=int, default=600)
     ap.add_argument("--seed", type=int, default=5)
+    ap.add_argument("--warm-iters", type=int, default=300)
+    ap.add_argument("--warm-width", type=float, default=8.0)
+    ap.add_argument("--warm-lr-s", type=float, default=1e-3)
+    ap.add_argument("--prefit-steps", type=int, default=300)
     args = ap.parse_args()
     from quantized_spectrum_cartography_amd import dip, maps, metrics, qmc, synthetic
     from quantized_spectrum_cartography_amd import quantization_model_log as qml
@@ -92,7 +96,70 @@ def main():
                          "map_nmse_log_zero_map": zero,
                          "cost_first": rd.costs_s[0], "cost_last": rd.costs_s[-1]}
         print(json.dumps({"c5_dip": out["c5_dip"]["map_nmse"][-1]}), file=sys.stderr, flush=True)
+    if args.warm_iters:
+        out.update(c5_warm_runs(Y, Wx, b, T, S_true, R, args))
     print(json.dumps(out), flush=True)
+
+
+def _nmse_pair(S, C, T, off):
+    from quantized_spectrum_cartography_amd import metrics
+    return (float(metrics.map_nmse(S, C, T)), float(metrics.map_nmse(S, C, T, log_offset=off)))
+
+
+def c5_warm_runs(Y, Wx, b, T, S_true, R, args):
+    """C5 from the de-quantized SPA warm start (warm.warm_start; the notebook's optional warm
+    start, qmc/qmc.ipynb :513-516): the warm start itself, then the DIP solver with its decoder
+    pre-fitted to the warm-start S and C initialised from the warm-start C (lr_c scaled to C)."""
+    from quantized_spectrum_cartography_amd import dip, metrics, warm
+    from quantized_spectrum_cartography_amd.utils import LOG_OFFSET_4
+    out = {}
+    K = Y.shape[0]
+    N = Y.shape[-1]
+    t0 = time.perf_counter()
+    S0, C0 = warm.warm_start(Y.cuda(), Wx.cuda(), b, 5.0, R, offset=LOG_OFFSET_4, log_model=True,
+                             width=args.warm_width)
+    torch.cuda.synchronize()
+    lin, lg = _nmse_pair(S0, C0, T, LOG_OFFSET_4)
+    out["c5_warm_start"] = {"width": args.warm_width, "map_nmse": lin, "map_nmse_log": lg,
+                            "slf_nmse": metrics.slf_nmse(S0, S_true),
+                            "wall_s": time.perf_counter() - t0}
+    print(json.dumps({"c5_warm_start": [lin, lg]}), file=sys.stderr, flush=True)
+    # DIP decoder pre-fitted to the warm-start fields (sigmoid output: fields scaled to peak 0.9)
+    smax = float(S0.max())
+    target = (S0 / smax * 0.9).reshape(R, 1, N, N).clamp(1e-4, 0.9)
+    dec = dip.make_decoder(N, N, seed=args.seed).cuda().train(False)
+    Z = torch.randn((R, 256), generator=torch.Generator().manual_seed(args.seed + 1)).cuda()
+    opt = torch.optim.Adam(dec.parameters(), lr=1e-3)
+    for _ in range(args.prefit_steps):
+        opt.zero_grad()
+        loss = torch.nn.functional.mse_loss(dec(Z).reshape(R, 1, N, N), target)
+        loss.backward()
+        opt.step()
+    with torch.no_grad():
+        Sd = dec(Z).reshape(R, 1, N, N)
+    C_init = C0 * (smax / 0.9)
+    lin_p, lg_p = _nmse_pair(Sd, C_init, T, LOG_OFFSET_4)
+    every = max(1, args.warm_iters // 12)
+    lr_c = 5e-3 * float(C_init.abs().mean()) / 0.1  # the notebook's lr_c at its C scale (~0.1)
+    t0 = time.perf_counter()
+    rd = dip.solve(Y, Wx, b, 5.0, R, offset=LOG_OFFSET_4, max_iter=args.warm_iters, decoder=dec,
+                   Z_init=Z, C_init=C_init.cpu(), lr_c=lr_c, lr_s=args.warm_lr_s,
+                   T_true=T, nmse_every=every)
+    torch.cuda.synchronize()
+    lin_f, lg_f = _nmse_pair(rd.S, rd.C, T, LOG_OFFSET_4)
+    out["c5_dip_warm"] = {"iters": args.warm_iters, "prefit_steps": args.prefit_steps,
+                          "lr_c": lr_c, "lr_s": args.warm_lr_s,
+                          "map_nmse_after_prefit": lin_p, "map_nmse_log_after_prefit": lg_p,
+                          "map_nmse": traj(rd, every),
+                          "map_nmse_best": min(([e * (i + 1), v] for i, v in
+                                                enumerate(rd.nmse) for e in [every]),
+                                               key=lambda x: x[1]) if rd.nmse else None,
+                          "map_nmse_final": lin_f, "map_nmse_log_final": lg_f,
+                          "slf_nmse": metrics.slf_nmse(rd.S, S_true),
+                          "wall_s": time.perf_counter() - t0,
+                          "cost_first": rd.costs_s[0], "cost_last": rd.costs_s[-1]}
+    print(json.dumps({"c5_dip_warm": [lin_f, lg_f]}), file=sys.stderr, flush=True)
+    return out
 
 
 if __name__ == "__main__":
