@@ -2334,18 +2334,22 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
   return QSC_OK;
 }
 
-// fused S-step + next C-pass: the C-pass tile partition (NP parts per bin list) of qsc_cpass
-static int cpass_parts(const qsc_obs_desc* d) {
+// fused S-step + next C-pass: the partition (parts per bin list) of the C-pass form qsc_cpass
+// uses for this layout -- the tile form's NP, or kCParts where qsc_cpass falls back to the
+// per-(tile, k-slice) form -- so that the fused launch sums every dC in the same order
+static int cpass_parts(const qsc_obs_desc* d, int R, bool sr) {
   const int nks = d->nks;
   int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
   const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
   while (NP > 1 && chunks / NP < 3.0) --NP;
-  return NP;
+  const bool tile = QSC_CPASS_TILE && nks * NP >= 4 &&
+                    cpass_tile_lds(d->PT, R, nks, NP, sr) <= 160 * 1024;
+  return tile ? NP : kCParts;
 }
 
 // the fused launch applies (its C-pass partition and LDS fit), with or without signed rows
 static bool scpass_fits(const qsc_obs_desc* d, int R, bool sr) {
-  const int NP = cpass_parts(d);
+  const int NP = cpass_parts(d, R, sr);
   const int U = d->nks * NP;
   // any unit count: small problems (C2: one 64-bin slice, ~13 entries per bin and tile, so one
   // unit per tile) run their C-pass units on the first waves while the rest wait at the end
@@ -2403,9 +2407,9 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
       ws_bytes < ws_bytes_for(d, R))
     return QSC_EINVAL;
   const int RP = rp_of(R);
-  const int NP = cpass_parts(d);
   const int kind = lik_kind(m);
   const bool sr = d->rowfmt == 1;
+  const int NP = cpass_parts(d, R, sr);
   if (!rowfmt_ok(d, R, kind)) return QSC_EINVAL;
   const size_t shm = scfused_lds(d->PT, R, d->K, d->nks, NP, sr);
   PassWs w = carve(d, R, ws);

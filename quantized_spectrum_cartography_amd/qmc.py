@@ -80,7 +80,7 @@ def _capture(solver, n, tolerant):
     except Exception as e:  # noqa: BLE001 - every failure takes the same clean-up path
         err = "%s: %s" % (type(e).__name__, e)
         del g
-        abandon_capture((s, caller))  # raises if a capture stays open
+        abandon_capture(s, caller)  # raises if the caller's stream is left capturing
         if not tolerant:
             raise
         solver.graph_error = err
@@ -122,22 +122,25 @@ def stream_capture_status(stream):
     return st.value if rc == 0 else -1  # -1: the query itself failed (treated as capturing)
 
 
-def abandon_capture(streams):
-    """End (and discard) any stream capture still open on `streams`, then synchronise the
-    device.  Raises RuntimeError if a capture cannot be ended."""
+def abandon_capture(side, caller):
+    """Clean up after a capture on `side` failed: end (and discard) the capture still open on
+    it, clear the HIP error state and synchronise the device.  HIP leaves a stream whose
+    capture was invalidated in the invalidated state for good (measured, tools/probe/
+    capture_fail.py: hipStreamEndCapture returns an error and the status stays 2), so the side
+    stream is abandoned -- captures always use a fresh one -- and only the caller's stream,
+    where eager work continues, must be out of capture.  Raises RuntimeError otherwise."""
     import ctypes
     h = _hip_lib()
-    for st in streams:
-        if stream_capture_status(st) != 0:
-            graph = ctypes.c_void_p(None)
-            h.hipStreamEndCapture(ctypes.c_void_p(st.cuda_stream), ctypes.byref(graph))
-            if graph.value:
-                h.hipGraphDestroy(graph)
+    if stream_capture_status(side) != 0:
+        graph = ctypes.c_void_p(None)
+        h.hipStreamEndCapture(ctypes.c_void_p(side.cuda_stream), ctypes.byref(graph))
+        if graph.value:
+            h.hipGraphDestroy(graph)
     h.hipGetLastError()  # clear the (non-sticky) capture error
-    still = [st for st in streams if stream_capture_status(st) != 0]
-    if still:
-        raise RuntimeError("a failed hipGraph capture left %d stream(s) capturing" % len(still))
+    if stream_capture_status(caller) != 0:
+        raise RuntimeError("a failed hipGraph capture left the caller's stream capturing")
     torch.cuda.synchronize()
+    h.hipGetLastError()
 
 
 def _upload(g):
