@@ -229,6 +229,17 @@ QSC_API int qsc_diff_sumsq(const float* a, const float* b, int64_t n, int32_t us
 QSC_API int qsc_map_diff_sumsq(const float* S, const float* C, const float* Ttrue, int32_t R,
                                int32_t P, int32_t K, int32_t use_log, double offset,
                                double* out2, void* ws, size_t ws_bytes, void* stream);
+/* the solver's NMSE history inside the iteration sequence (NMSE(get_tensor(S, C), T_true) after
+ * every S-step, qmc/qmc.ipynb :582, :637): with the state's iteration counter it = st->iter,
+ * when it % every == 0 writes hist[2*(it/every - 1) + {0, 1}] = {sum (T_hat - T)^2, sum T^2}
+ * (slots < cap), otherwise does nothing -- so it can be captured into every iteration of a
+ * replayed hipGraph.  S_pos is the passes' position-order S [Pp][RP]; iperm[p] = the position
+ * of pixel p (the inverse of qsc_obs_order's perm). */
+QSC_API int qsc_map_nmse_track(const float* S_pos, const int32_t* iperm, int32_t RP,
+                               const float* C, const float* Ttrue, int32_t R, int32_t P,
+                               int32_t K, int32_t use_log, double offset, const qsc_state* st,
+                               int32_t every, double* hist, int32_t cap, void* ws,
+                               size_t ws_bytes, void* stream);
 /* out[0] = sum x^2 (fp32 result, fixed order) */
 QSC_API int qsc_sumsq(const float* x, int64_t n, float* out, void* ws, size_t ws_bytes,
                       void* stream);

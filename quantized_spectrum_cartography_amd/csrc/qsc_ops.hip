@@ -302,6 +302,70 @@ __global__ void __launch_bounds__(kBlock) map_diff_sumsq_kernel(
   }
 }
 
+// the solver's map NMSE history (qmc/qmc.ipynb :582, :637: NMSE(get_tensor(S, C), T_true) every
+// iteration) inside the captured iteration sequence: S in the passes' position order (pixel p's
+// row at position iperm[p]), run only when the device iteration counter is a multiple of
+// `every` (all blocks exit otherwise, so the launch can sit in every iteration of a hipGraph)
+template <int RM>
+__global__ void __launch_bounds__(kBlock) map_track_kernel(
+    const float* __restrict__ Sp, const int* __restrict__ iperm, int RP,
+    const float* __restrict__ C, const float* __restrict__ Tt, int R, int P, int K, int use_log,
+    float off, const qsc_state* __restrict__ st, int every, double* __restrict__ part) {
+  __shared__ double sh[kBlock / 64];
+  const int it = st->iter;
+  if (every <= 0 || it <= 0 || it % every != 0) return;
+  double s0 = 0.0, s1 = 0.0;
+  const int64_t n = (int64_t)P * K;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = i / P, p = i - k * P;
+    const float* row = Sp + (int64_t)iperm[p] * RP;
+    float t = 0.0f;
+#pragma unroll
+    for (int r = 0; r < RM; ++r)
+      if (r < R) {
+        const float pr = __fmul_rn(row[r], C[(int64_t)r * K + k]);
+        t = (r == 0) ? pr : __fadd_rn(t, pr);
+      }
+    float y = Tt[i];
+    if (use_log) {
+      t = logf(t + off);
+      y = logf(y + off);
+    }
+    const double d = (double)t - (double)y;
+    s0 += d * d;
+    s1 += (double)y * (double)y;
+  }
+  const double r0 = block_sum(s0, sh);
+  const double r1 = block_sum(s1, sh);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = r0;
+    part[2 * blockIdx.x + 1] = r1;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) track_finish_kernel(const double* __restrict__ part,
+                                                              int nparts,
+                                                              const qsc_state* __restrict__ st,
+                                                              int every, double* __restrict__ hist,
+                                                              int cap) {
+  __shared__ double sh[kBlock / 64];
+  const int it = st->iter;
+  if (every <= 0 || it <= 0 || it % every != 0) return;
+  double s0 = 0.0, s1 = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+    s0 += part[2 * i];
+    s1 += part[2 * i + 1];
+  }
+  const double r0 = block_sum(s0, sh);
+  const double r1 = block_sum(s1, sh);
+  const int slot = it / every - 1;
+  if (threadIdx.x == 0 && slot < cap) {
+    hist[2 * slot] = r0;
+    hist[2 * slot + 1] = r1;
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) finish_pairs_kernel(const double* __restrict__ part,
                                                               int nparts,
                                                               double* __restrict__ out2) {
@@ -565,6 +629,24 @@ QSC_API int qsc_map_diff_sumsq(const float* S, const float* C, const float* Ttru
   QSC_CHECK_LAUNCH();
   hipLaunchKernelGGL(finish_pairs_kernel, dim3(1), dim3(kBlock), 0, STREAM(stream), part,
                      kReduceBlocks, out2);
+  QSC_CHECK_LAUNCH();
+  return QSC_OK;
+}
+
+QSC_API int qsc_map_nmse_track(const float* S_pos, const int32_t* iperm, int32_t RP,
+                               const float* C, const float* Ttrue, int32_t R, int32_t P,
+                               int32_t K, int32_t use_log, double offset, const qsc_state* st,
+                               int32_t every, double* hist, int32_t cap, void* ws,
+                               size_t ws_bytes, void* stream) {
+  if (R < 1 || R > QSC_MAX_R || RP < R || P < 1 || K < 1 || !S_pos || !iperm || !C || !Ttrue ||
+      !st || every < 1 || !hist || cap < 0 || !ws || ws_bytes < qsc_reduce_workspace_bytes(0))
+    return QSC_EINVAL;
+  double* part = (double*)ws;
+  DISPATCH_R(R, map_track_kernel, dim3(kReduceBlocks), dim3(kBlock), STREAM(stream), S_pos,
+             iperm, RP, C, Ttrue, R, P, K, use_log, (float)offset, st, every, part);
+  QSC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(track_finish_kernel, dim3(1), dim3(kBlock), 0, STREAM(stream), part,
+                     kReduceBlocks, st, every, hist, cap);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }

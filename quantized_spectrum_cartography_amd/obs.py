@@ -202,6 +202,17 @@ class Observations:
             raise ValueError("rank R must be in [1, %d]" % _lib.QSC_MAX_R)
         return rp
 
+    def iperm(self):
+        """(P,) int32: the position of every pixel (inverse of perm; cached)."""
+        ip = getattr(self, "_iperm", None)
+        if ip is None:
+            ip = torch.full((self.P,), -1, dtype=torch.int32, device=self.device)
+            valid = self.perm >= 0
+            ip[self.perm[valid].long()] = torch.arange(self.Pp, dtype=torch.int32,
+                                                       device=self.device)[valid]
+            self._iperm = ip
+        return ip
+
     def to_positions(self, X):
         """(R, P) natural pixel order -> (Pp, RP) position order (pixel-major rows, zero padded)."""
         R = X.shape[0]

@@ -209,7 +209,8 @@ class FreeSSolver:
     """
 
     def __init__(self, obs, S_init, C_init, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
-                 betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024, fuse=True):
+                 betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024, fuse=True,
+                 T_true=None, nmse_every=0):
         self.obs = obs
         R = S_init.shape[0]
         self.R = R
@@ -224,6 +225,17 @@ class FreeSSolver:
         self.engine.init_state(self.S)
         self.fuse = bool(fuse) and self.engine.scpass_supported()
         self._graphs = {}
+        # map NMSE after every `nmse_every`-th S-step, on the device inside the iteration
+        # sequence (qsc_map_nmse_track; the reference evaluates it every iteration, :582, :637)
+        self.nmse_every = int(nmse_every) if T_true is not None else 0
+        if self.nmse_every:
+            K, P = obs.K, obs.P
+            self._T = _dev(T_true.detach().to(torch.float32)).reshape(K, P).contiguous()
+            self._iperm = obs.iperm()
+            self._nmse_hist = torch.zeros((max(hist_cap // self.nmse_every, 1), 2),
+                                          dtype=torch.float64, device=self.S.device)
+            self._nmse_ws = torch.empty(_lib.lib().qsc_reduce_workspace_bytes(0),
+                                        dtype=torch.uint8, device=self.S.device)
 
     # one outer iteration = C grad-step + S grad-step
     def c_step(self):
@@ -234,6 +246,7 @@ class FreeSSolver:
     def s_step(self):
         e = self.engine
         e.spass(self.S, self.C, 1, mS=self.mS, vS=self.vS, adam=self.adam_s, lambda_s=self.lambda_s)
+        self._track()
 
     def iteration(self):
         self.c_step()
@@ -243,7 +256,26 @@ class FreeSSolver:
         """S-step i fused with C-pass i+1, then C-step i+1's finish (needs a C-step before)."""
         e = self.engine
         e.scpass(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s)
+        self._track()  # (S_{i+1}, C_{i+1}): C is updated by the cfinish below
         e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)
+
+    def _track(self):
+        if not self.nmse_every:
+            return
+        o = self.obs
+        _lib.call("qsc_map_nmse_track", _lib.ptr(self.S), _lib.ptr(self._iperm), self.S.shape[1],
+                  _lib.ptr(self.C), _lib.ptr(self._T), self.R, o.P, o.K, 0, 0.0,
+                  _lib.ptr(self.engine.state), self.nmse_every, _lib.ptr(self._nmse_hist),
+                  self._nmse_hist.shape[0], _lib.ptr(self._nmse_ws), self._nmse_ws.numel(),
+                  _lib.stream())
+
+    def nmse_history(self):
+        """Map NMSE after S-steps nmse_every, 2 nmse_every, ... recorded so far."""
+        if not self.nmse_every:
+            return []
+        n = min(int(self.state()["iter"]) // self.nmse_every, self._nmse_hist.shape[0])
+        h = self._nmse_hist[:n].cpu()
+        return [float((a / b) ** 0.5) if b > 0 else float("nan") for a, b in h.tolist()]
 
     def issue(self, n):
         """Enqueue the kernel sequence of n outer iterations (no host sync)."""
@@ -313,19 +345,20 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
     if generator is None:
         if S_init is None:
             S_init = torch.zeros(R, 1, I, J)
+        # the NMSE history is recorded on the device inside the run (no host round trips);
+        # a callback still gets control every nmse_every iterations (or once at the end)
         sol = FreeSSolver(obs, S_init, C_init, lambda_c, lambda_s, lr_c, lr_s, betas, eps,
-                          project_c, hist_cap=max_iter, fuse=fuse)
-        nmse = []
+                          project_c, hist_cap=max_iter, fuse=fuse,
+                          T_true=T_true if nmse_every else None, nmse_every=nmse_every)
         done = 0
-        chunk = nmse_every if (nmse_every and T_true is not None) else max_iter
+        chunk = nmse_every if (callback is not None and nmse_every) else max_iter
         while done < max_iter:
             n = min(chunk, max_iter - done)
             sol.run(n, use_graph=use_graph)
             done += n
-            if T_true is not None and nmse_every:
-                nmse.append(map_nmse(sol.S_pixels(), sol.C, T_true))
             if callback is not None:
                 callback(done, sol)
+        nmse = sol.nmse_history()
         costs_c, costs_s = sol.history()
         return SolveResult(S=sol.S_pixels(), C=sol.C.clone(), costs_c=costs_c, costs_s=costs_s,
                            nmse=nmse, iters=max_iter, fused=sol.fuse)

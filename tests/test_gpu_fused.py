@@ -447,3 +447,23 @@ def test_other_rank_engine_does_not_invalidate_captured_graph():
     sol.run(3, use_graph=True)  # replays the graph captured before
     assert np.array_equal(ref.S.cpu().numpy(), sol.S.cpu().numpy())
     assert np.array_equal(ref.C.cpu().numpy(), sol.C.cpu().numpy())
+
+
+def test_device_nmse_history_matches_host_nmse():
+    """The per-iteration map NMSE (qmc/qmc.ipynb :582, :637) recorded on the device inside the
+    captured run (qsc_map_nmse_track) equals NMSE(get_tensor(S, C), T_true) evaluated on the
+    host between chunks of the same run."""
+    from quantized_spectrum_cartography_amd import qmc
+    from quantized_spectrum_cartography_amd._model import map_nmse
+    from quantized_spectrum_cartography_amd.obs import Observations
+    d = _random_case(54, 4, 64, 64, 64)
+    o = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=4, tile=512)
+    res = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], S_init=d["S0"], C_init=d["C0"],
+                    max_iter=12, obs=o, T_true=d["T"], nmse_every=3, use_graph=True)
+    assert len(res.nmse) == 4
+    sol = qmc.FreeSSolver(o, d["S0"], d["C0"], hist_cap=16)
+    ref = []
+    for _ in range(4):
+        sol.run(3)
+        ref.append(map_nmse(sol.S_pixels(), sol.C, d["T"]))
+    assert np.allclose(res.nmse, ref, rtol=1e-12, atol=0), (res.nmse, ref)
