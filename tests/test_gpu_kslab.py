@@ -70,3 +70,22 @@ def test_slice_nsq_rebuilds_the_update_partials():
     a.slice_nsq(S)
     torch.cuda.synchronize()
     assert torch.equal(n0, a.ws)
+
+
+def test_adam_moments_flush_denormals_documented_deviation():
+    """The pass library runs with f32 denormals flushed (the one-bit tail saturation relies on
+    it), and its fused Adam epilogues share the setting: moments in the denormal
+    range (|m| < 2^-126) are read and written as 0, where torch.optim.Adam on the CPU would keep
+    them.  This pins the deviation; it cannot move S: an update of such a moment is
+    below 1e-30 * lr, far under one ulp of any S value the solver carries."""
+    obs, S, dS, mS, vS, adam, R, PassEngine = _setup(R=4, seed=93)
+    e = PassEngine(obs, R)
+    e.init_state(S)
+    mS[:, :R] = 1e-39          # denormal
+    vS[:, :R] = 1e-39
+    dS.zero_()
+    S0 = S.clone()
+    e.supdate(S, mS, vS, dS, adam, 0.0)
+    torch.cuda.synchronize()
+    assert torch.count_nonzero(mS).item() == 0 and torch.count_nonzero(vS).item() == 0
+    assert torch.equal(S, S0)
