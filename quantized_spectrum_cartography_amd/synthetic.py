@@ -139,4 +139,7 @@ CONFIGS = {
     "c2": (256, 256, 64, 4),
     "c3": (512, 512, 256, 8),
     "c4": (512, 512, 1024, 16),
+    # one GPU's K-slab share of c4 at N = 8 (K_loc = 1024 / 8): the per-GPU kernel of the
+    # north-star 8-GPU layout, benchable on one GPU
+    "c4k": (512, 512, 128, 16),
 }
