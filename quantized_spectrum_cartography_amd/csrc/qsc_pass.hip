@@ -1107,11 +1107,12 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   // 1. entry read-ahead of this wave's part of the lists and C[:, k], before the staging
   const int64_t wi = (int64_t)t * nks + ks;
   const int W4 = width[wi] >> 2;
-  const int j0 = (W4 * part) / kCParts, j1 = (W4 * (part + 1)) / kCParts;
+  // strided parts: part p walks chunks p, p + kCParts, ... (the partition of every C-pass form)
+  const int j0 = part, j1 = W4;
   const V4* src = reinterpret_cast<const V4*>(ent + off[wi]);
   const uint32_t lo = (uint32_t)lane * (uint32_t)sizeof(V4);
   V4 buf[kGroup];
-  load_group(src, lo, 64, j0, 1, max(j1 - 1, 0), buf);
+  load_group(src, lo, 64, j0, kCParts, max(j1 - 1, 0), buf);
   const int k = kmap[wi * 64 + lane];  // this lane's bin (count-sorted order, include/qsc.h)
   float cv[RP];
 #pragma unroll
@@ -1147,9 +1148,9 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
   f2v nll = splat2(0.0f);
 #if QSC_CPASS_MASKED
-  walk_masked<RP, E, KIND, LOG>(src, lo, 64, j0, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+  walk_masked<RP, E, KIND, LOG>(src, lo, 64, j0, j0, j1, kCParts, buf, own, Sl, El, lk, accp, nll);
 #else
-  walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+  walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, kCParts, buf, own, Sl, El, lk, accp, nll);
 #endif
   STAMP(wg, 2);
   const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
@@ -1235,11 +1236,11 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
     const int ks = uu / NP, part = uu - ks * NP;
     wi = t * nks + ks;
     const int W4 = width[wi] >> 2;
-    j0 = (W4 * part) / NP;
-    j1 = (W4 * (part + 1)) / NP;
+    j0 = part;  // strided parts: chunks part, part + NP, ...
+    j1 = W4;
     src = reinterpret_cast<const V4*>(ent + off[wi]);
     QSC_DCHECK(off[wi] + (int64_t)width[wi] * 64 <= lk.dbg_ent[1]);
-    load_group(src, lo, 64, j0, 1, max(j1 - 1, 0), buf);
+    load_group(src, lo, 64, j0, NP, max(j1 - 1, 0), buf);
     k = kmap[wi * 64 + lane];  // this lane's bin (count-sorted order)
     QSC_DCHECK(k >= 0 && k < Kp);
 #pragma unroll
@@ -1274,7 +1275,7 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, NP, buf, own, Sl, El, lk, accp, nll);
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (NP == 1) {
       // the unit is the whole (tile, k-slice): its slab rows straight from registers
@@ -1368,7 +1369,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
     const float* __restrict__ C, float* __restrict__ mS, float* __restrict__ vS, qsc_adam ad,
     float lambda_s, qsc_state* __restrict__ st, float* __restrict__ part_nll_s,
     float* __restrict__ part_nsq_s, float* __restrict__ slab, float* __restrict__ part_nll_c,
-    float* __restrict__ cnsq, AdamCache* __restrict__ acache) {
+    float* __restrict__ cnsq, AdamCache* __restrict__ acache, const int* __restrict__ c_split) {
   using V4 = typename Ent<E>::V4;
   constexpr int CP = TP<RP, KIND>::v;  // C^T row pitch == S tile row pitch
   constexpr int RH = RP / 2;
@@ -1613,18 +1614,6 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
     ++n;
     return more;
   };
-  if (il < nsl) {
-    SliceIn<RP, E, ADAM> nxt;
-    for (;;) {
-      if (!one_slice(cur, nxt)) break;
-      if (!one_slice(nxt, cur)) break;
-    }
-  }
-
-  // the next launch's S-step scalars, by the oldest wave of block 0 (it has slack: its slices
-  // are done long before the tile barrier)
-  if (blockIdx.x == 0 && threadIdx.x == 0) adam_cache_store(acache, ad, step_s + 2);
-
   // 3. C-pass units of the tile at the new S (cpass_tile_kernel steps 1, 3, 4)
   int u = w;
   V4 buf[kGroup];
@@ -1636,20 +1625,99 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
     const int ks = uu / NP, part = uu - ks * NP;
     wi = t * nks + ks;
     const int W4 = c_width[wi] >> 2;
-    j0 = (W4 * part) / NP;
-    j1 = (W4 * (part + 1)) / NP;
+    j0 = part;  // strided parts: chunks part, part + NP, ...
+    j1 = W4;
     src = reinterpret_cast<const V4*>(c_ent + c_off[wi]);
     QSC_DCHECK(c_off[wi] + (int64_t)c_width[wi] * 64 <= lk.dbg_ent[1]);
-    load_group(src, lo, 64, j0, 1, max(j1 - 1, 0), buf);
+    load_group(src, lo, 64, j0, NP, max(j1 - 1, 0), buf);
     k = c_kmap[wi * 64 + lane];  // this lane's bin (count-sorted order)
     QSC_DCHECK(k >= 0 && k < Kp);
 #pragma unroll
     for (int r = 0; r < RP; ++r) cv[r] = Cl[min(k, K - 1) * CP + r];  // C_i, as the S-step used
   };
+  // Phase split (c_split, qsc_obs_split; one C-pass unit per wave and >= 2 S-step rounds): the
+  // first S-step round updates tile rows [0, NW*QSC_SLICE); every list's chunks j < m hold only
+  // such rows, so right after that round the unit walks its chunks < m (phase A) while the
+  // second round's slice reads are still in flight, and its chunks >= m after the last round
+  // (phase B), continuing the same accumulators: the same sums in the same order as the
+  // unsplit walk, with part of the C-pass arithmetic overlapping the S-step's HBM traffic.
+  const bool split = c_split != nullptr && U <= NW && nsl >= 2 * NW;
+  f2v sp_own[RP / 2], sp_acc[RP / 2], sp_nll = splat2(0.0f);
+  int sp_m = 0;
+  if (il < nsl) {
+    SliceIn<RP, E, ADAM> nxt;
+    bool go = true;
+    if (split) {
+      go = one_slice(cur, nxt);  // round 1: rows [0, NW*QSC_SLICE); round 2's reads in flight
+      __syncthreads();
+      STAMP(wg, 15);
+      if (u < U) {
+        unit_begin(u);
+        sp_m = c_split[wi];
+#pragma unroll
+        for (int j = 0; j < RP / 2; ++j) {
+          sp_own[j] = f2v{(2 * j < R && k < K) ? cv[2 * j] : 0.0f,
+                          (2 * j + 1 < R && k < K) ? cv[2 * j + 1] : 0.0f} * splat2(own_scale);
+          sp_acc[j] = splat2(0.0f);
+        }
+        walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, min(sp_m, j1), NP, buf, sp_own, Sl, El, lk,
+                                      sp_acc, sp_nll);
+      }
+      STAMP(wg, 16);
+      if (go) {
+        for (;;) {
+          if (!one_slice(nxt, cur)) break;
+          if (!one_slice(cur, nxt)) break;
+        }
+      }
+    } else {
+      for (;;) {
+        if (!one_slice(cur, nxt)) break;
+        if (!one_slice(nxt, cur)) break;
+      }
+    }
+  }
+
+  // the next launch's S-step scalars, by the oldest wave of block 0 (it has slack: its slices
+  // are done long before the tile barrier)
+  if (blockIdx.x == 0 && threadIdx.x == 0) adam_cache_store(acache, ad, step_s + 2);
+
   STAMP(wg, 2);
-  if (u < U) unit_begin(u);
-  __syncthreads();  // the whole S tile is in LDS
-  STAMP(wg, 3);
+  if (split) {
+    // phase B: the unit's chunks >= m (the first of its stride at or past m)
+    int jB = j0;
+    if (u < U) {
+      jB = j0 + ((max(sp_m - j0, 0) + NP - 1) / NP) * NP;
+      load_group(src, lo, 64, jB, NP, max(j1 - 1, 0), buf);
+    }
+    __syncthreads();  // the whole S tile is in LDS
+    STAMP(wg, 3);
+    if (u < U) {
+      walk_groups<RP, E, KIND, LOG>(src, lo, 64, jB, j1, NP, buf, sp_own, Sl, El, lk, sp_acc,
+                                    sp_nll);
+      const float nll_w = wave_sum_dpp(sp_nll.x + sp_nll.y) * kLn2;
+      if (NP == 1) {
+#pragma unroll
+        for (int j = 0; j < RP / 2; ++j) {
+          if (2 * j < R) slab[((int64_t)t * R + 2 * j) * Kp + k] = sp_acc[j].x;
+          if (2 * j + 1 < R) slab[((int64_t)t * R + 2 * j + 1) * Kp + k] = sp_acc[j].y;
+        }
+        if (lane == 0) part_nll_c[wi] = nll_w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < RP / 2; ++j) {
+          if (2 * j < R) Pl[((size_t)u * R + 2 * j) * 64 + lane] = sp_acc[j].x;
+          if (2 * j + 1 < R) Pl[((size_t)u * R + 2 * j + 1) * 64 + lane] = sp_acc[j].y;
+        }
+        if (lane == 0) Nl[u] = nll_w;
+      }
+    }
+    u = U;  // (the unsplit unit loop below has nothing left)
+  } else {
+    if (u < U) unit_begin(u);
+    __syncthreads();  // the whole S tile is in LDS
+    STAMP(wg, 3);
+  }
   for (; u < U; u += NW) {
     f2v own[RP / 2];
 #pragma unroll
@@ -1660,7 +1728,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, 1, buf, own, Sl, El, lk, accp, nll);
+    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, NP, buf, own, Sl, El, lk, accp, nll);
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (NP == 1) {
 #pragma unroll
@@ -2396,10 +2464,25 @@ QSC_API int qsc_scpass_supported(const qsc_obs_desc* d, int32_t R) {
   return scpass_fits(d, R, d->rowfmt == 1) ? 1 : 0;
 }
 
+// threads of the fused launch at rank R (waves: two S-step slices each, 4..16; 4..8 at rank 16)
+static unsigned scpass_threads(const qsc_obs_desc* d, int R) {
+  const int nsl = d->PT / QSC_SLICE;
+  return 64u * (unsigned)std::min(rp_of(R) > 8 ? 8 : QSC_FUSED_WAVES, std::max(4, nsl / 2));
+}
+
+QSC_API int32_t qsc_scpass_split_rows(const qsc_obs_desc* d, int32_t R) {
+  if (!desc_ok(d) || R < 1 || R > QSC_MAX_R) return 0;
+  const int NW = (int)(scpass_threads(d, R) / 64), nsl = d->PT / QSC_SLICE;
+  const int NP = cpass_parts(d, R, d->rowfmt == 1);
+  if (nsl < 2 * NW || d->nks * NP > NW) return 0;  // the split needs one unit per wave
+  return NW * QSC_SLICE;
+}
+
 QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
                        const int64_t* s_off, const void* c_entries, const int32_t* c_width,
-                       const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m, int32_t R,
-                       float* S, const float* C, float* mS, float* vS, const qsc_adam* adam,
+                       const int64_t* c_off, const int32_t* c_kmap, const int32_t* c_split,
+                       int32_t split_rows, const qsc_model* m, int32_t R, float* S,
+                       const float* C, float* mS, float* vS, const qsc_adam* adam,
                        float lambda_s, qsc_state* st, void* ws, size_t ws_bytes, void* stream) {
   if (!qsc_scpass_supported(d, R) || !m || m->nbounds - 1 != d->nbins || !S || !C || !mS ||
       !vS || !adam || !st || !s_width || !s_off || !c_width || !c_off || !c_kmap ||
@@ -2422,10 +2505,11 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
   else if (!m->log_model)
     scale_edges(&E, m->nbounds - 1, lk.a);
   const qsc_adam ad = *adam;
-  // waves: two S-step slices each (the tile's nsl slices), 4..16 (4..8 at rank 16)
-  const int nsl = d->PT / QSC_SLICE;
-  const unsigned threads =
-      64u * (unsigned)std::min(RP > 8 ? 8 : QSC_FUSED_WAVES, std::max(4, nsl / 2));
+  const unsigned threads = scpass_threads(d, R);
+  (void)RP;
+  // the phase split applies only to lists split for exactly this launch's first S-step round
+  const int* split = (c_split && split_rows > 0 && split_rows == qsc_scpass_split_rows(d, R))
+                         ? c_split : nullptr;
   hipStream_t s = STREAM(stream);
 #define SCPASS_LAUNCH(RPV, ET, KD, LG)                                                         \
   do {                                                                                         \
@@ -2433,7 +2517,7 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
                          dim3(threads), shm, s, (const ET*)s_entries, s_width, s_off,         \
                          (const ET*)c_entries, c_width, c_off, c_kmap, d->nks, NP, d->PT, lk, E, \
                          d->nbins, R, d->K, S, C, mS, vS, ad, lambda_s, st, w.snll, w.snsq,    \
-                         w.slab, w.cnll, w.cnsq, w.acache);                                    \
+                         w.slab, w.cnll, w.cnsq, w.acache, split);                             \
   } while (0)
   QSC_DISPATCH_PASS(SCPASS_LAUNCH);
 #undef SCPASS_LAUNCH

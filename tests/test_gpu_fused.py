@@ -155,7 +155,9 @@ def test_solver_graph_replay_matches_eager():
                           (51, 16, 64, 64, 128, True, "probit", 2, 512),
                           # one C-pass unit per tile (C2 shape class: K = 64, 128-position tiles)
                           (52, 4, 64, 64, 64, False, "probit", 2, 128),
-                          (53, 4, 96, 64, 64, False, "probit", 2, None)])
+                          (53, 4, 96, 64, 64, False, "probit", 2, None),
+                          # C3 shape class at 1024-position tiles: the phase-split fused launch
+                          (55, 8, 128, 128, 256, False, "probit", 2, 1024)])
 def test_fused_spass_cpass_bitexact(seed, R, I, J, K, log_model, loss, nbins, tile):
     """qsc_scpass (S-step + next C-pass in one launch) reproduces spass + cpass bit for bit:
     S, C and the cost history after n iterations, eager and hipGraph."""
@@ -467,3 +469,27 @@ def test_device_nmse_history_matches_host_nmse():
         sol.run(3)
         ref.append(map_nmse(sol.S_pixels(), sol.C, d["T"]))
     assert np.allclose(res.nmse, ref, rtol=1e-12, atol=0), (res.nmse, ref)
+
+
+def test_phase_split_fused_launch_is_bitexact():
+    """The phase-split fused launch (C-pass chunks j < c_split walked right after the first
+    S-step round, include/qsc.h qsc_scpass) gives the unsplit launch's S, C and costs bit for
+    bit, and the split really applies at the C3 shape class."""
+    from quantized_spectrum_cartography_amd import qmc
+    from quantized_spectrum_cartography_amd.obs import Observations
+    d = _random_case(56, 8, 128, 128, 256)
+    o = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=8, tile=1024)
+    assert o.split_rows == 16 * 32 and int(o.c_split.min()) > 0
+    kw = dict(S_init=d["S0"], C_init=d["C0"], max_iter=9)
+    a = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], obs=o, **kw)
+    # the same lists launched without the split (engines pass c_split only when the layout's
+    # split_rows matches their launch)
+    rows, o.split_rows = o.split_rows, 0
+    try:
+        b = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], obs=o, **kw)
+    finally:
+        o.split_rows = rows
+    assert a.fused and b.fused
+    assert np.array_equal(a.S.cpu().numpy(), b.S.cpu().numpy())
+    assert np.array_equal(a.C.cpu().numpy(), b.C.cpu().numpy())
+    assert a.costs_c == b.costs_c and a.costs_s == b.costs_s
