@@ -73,9 +73,32 @@ constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 #ifndef QSC_KMAP_PF
 #define QSC_KMAP_PF 1
 #endif
+// fused launch: the phase split (scfused, section 3).  Off by default: its phase-A walk sits
+// between the first S-step round and the rest with the next slice's reads in flight, and at
+// 128 VGPRs (16 waves per CU) that spills (24-115 VGPRs across the instantiations); unsplit,
+// the rank-8 kernels allocate <= 128 with none
+#ifndef QSC_PHASE_SPLIT
+#define QSC_PHASE_SPLIT 0
+#endif
+// C-pass parts: part p of np walks a contiguous block of its list's chunks, or (strided, which
+// the phase split needs) chunks p, p + np, ...; every C-pass form uses the one partition, so
+// their sums agree bit for bit
+#ifndef QSC_STRIDED_PARTS
+#define QSC_STRIDED_PARTS QSC_PHASE_SPLIT
+#endif
+#if QSC_PHASE_SPLIT && !QSC_STRIDED_PARTS
+#error "the phase split needs strided C-pass parts"
+#endif
 #ifndef QSC_CPASS_WAVES
 #define QSC_CPASS_WAVES 4
 #endif
+struct PartRange {
+  int j0, j1, js;  // chunks j0, j0 + js, ... < j1
+};
+__device__ inline PartRange part_range(int W4, int p, int np) {
+  return QSC_STRIDED_PARTS ? PartRange{p, W4, np}
+                           : PartRange{(W4 * p) / np, (W4 * (p + 1)) / np, 1};
+}
 template <int RP, int W>
 struct Occ {
   static constexpr int v = (RP > 8) ? (W > 4 ? 4 : W) : W;
@@ -411,8 +434,22 @@ __device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const f2v (&
                                       f2v (&acc)[RP / 2], f2v& nll, bool valid = true) {
   uint32_t e[4];
   Ent<E>::unpack(v, e);
-  pair_step<RP, E, KIND, LOG, 1>(e[0], e[1], own, tab, edges, lk, acc, nll, valid);
-  pair_step<RP, E, KIND, LOG, 1>(e[2], e[3], own, tab, edges, lk, acc, nll, valid);
+  if constexpr (is_sr(KIND)) {
+    // the software-pipelined walk's arithmetic exactly (one v_log of the chunk's four P), so
+    // the C-pass NLL is the same whichever walk form evaluates a chunk
+    f2v oa[RP / 2], ob[RP / 2], tha, thb, pqa, pqb;
+    pair_rows<RP, E, KIND, 1>(e[0], e[1], own, tab, oa, ob, tha, thb, lk);
+    pair_math<RP, E, KIND, LOG>(e[0], e[1], own, oa, ob, tha, thb, edges, lk, acc, nll, pqa,
+                                valid);
+    pair_rows<RP, E, KIND, 1>(e[2], e[3], own, tab, oa, ob, tha, thb, lk);
+    pair_math<RP, E, KIND, LOG>(e[2], e[3], own, oa, ob, tha, thb, edges, lk, acc, nll, pqb,
+                                valid);
+    const f2v pp = pqa * pqb;
+    nll.x -= __builtin_amdgcn_logf(pp.x * pp.y);
+  } else {
+    pair_step<RP, E, KIND, LOG, 1>(e[0], e[1], own, tab, edges, lk, acc, nll, valid);
+    pair_step<RP, E, KIND, LOG, 1>(e[2], e[3], own, tab, edges, lk, acc, nll, valid);
+  }
 }
 
 // half a chunk (the S-pass lane's unit: the pixel's two lanes split every chunk)
@@ -446,7 +483,7 @@ __device__ __forceinline__ void load_group(const V4* __restrict__ src, uint32_t 
 
 // Consume group b (chunks jb, jb+js, ..., < j1), then walk the rest of the list with the next
 // group's loads issued ahead of the current group's arithmetic.
-template <int RP, typename E, int KIND, bool LOG>
+template <int RP, typename E, int KIND, bool LOG, bool PFC = (QSC_ROW_PF_C != 0)>
 __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restrict__ src,
                                             uint32_t lo, int row, int jb, int j1, int js,
                                             typename Ent<E>::V4 (&b)[kGroup],
@@ -456,7 +493,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
                                             f2v (&acc)[RP / 2], f2v& nll) {
   using V4 = typename Ent<E>::V4;
   const int jlast = max(j1 - 1, 0);
-#if QSC_ROW_PF_C
+  if constexpr (PFC) {
   // software-pipelined gather: the LDS rows of the next entry pair are read before the current
   // pair's arithmetic, so the LDS latency runs under it (the group's chunks are loaded, clamped,
   // so a prefetch past the list end reads valid rows that are never used)
@@ -467,13 +504,11 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
     Ent<E>::unpack(b[0], e);
     pair_rows<RP, E, KIND, 1>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
   }
-#endif
   for (;;) {
     const int jn = jb + kGroup * js;
     const bool more = jn < j1;
     V4 nb[kGroup];
     load_group(src, lo, row, jn, js, jlast, nb);  // unconditional: static vmcnt accounting
-#if QSC_ROW_PF_C
 #pragma unroll
     for (int i = 0; i < kGroup; ++i)
       if (jb + i * js < j1) {
@@ -504,15 +539,22 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
       Ent<E>::unpack(b[0], e);
       pair_rows<RP, E, KIND, 1>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
     }
-#else
+    jb = jn;
+  }
+  } else {
+  for (;;) {
+    const int jn = jb + kGroup * js;
+    const bool more = jn < j1;
+    V4 nb[kGroup];
+    load_group(src, lo, row, jn, js, jlast, nb);  // unconditional: static vmcnt accounting
 #pragma unroll
     for (int i = 0; i < kGroup; ++i)
       if (jb + i * js < j1) chunk<RP, E, KIND, LOG>(b[i], own, tab, edges, lk, acc, nll);
     if (!more) break;
 #pragma unroll
     for (int i = 0; i < kGroup; ++i) b[i] = nb[i];
-#endif
     jb = jn;
+  }
   }
 }
 
@@ -1107,12 +1149,12 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   // 1. entry read-ahead of this wave's part of the lists and C[:, k], before the staging
   const int64_t wi = (int64_t)t * nks + ks;
   const int W4 = width[wi] >> 2;
-  // strided parts: part p walks chunks p, p + kCParts, ... (the partition of every C-pass form)
-  const int j0 = part, j1 = W4;
+  const PartRange pr = part_range(W4, part, kCParts);
+  const int j0 = pr.j0, j1 = pr.j1;
   const V4* src = reinterpret_cast<const V4*>(ent + off[wi]);
   const uint32_t lo = (uint32_t)lane * (uint32_t)sizeof(V4);
   V4 buf[kGroup];
-  load_group(src, lo, 64, j0, kCParts, max(j1 - 1, 0), buf);
+  load_group(src, lo, 64, j0, pr.js, max(j1 - 1, 0), buf);
   const int k = kmap[wi * 64 + lane];  // this lane's bin (count-sorted order, include/qsc.h)
   float cv[RP];
 #pragma unroll
@@ -1148,9 +1190,9 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
   for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
   f2v nll = splat2(0.0f);
 #if QSC_CPASS_MASKED
-  walk_masked<RP, E, KIND, LOG>(src, lo, 64, j0, j0, j1, kCParts, buf, own, Sl, El, lk, accp, nll);
+  walk_masked<RP, E, KIND, LOG>(src, lo, 64, j0, j0, j1, pr.js, buf, own, Sl, El, lk, accp, nll);
 #else
-  walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, kCParts, buf, own, Sl, El, lk, accp, nll);
+  walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, pr.js, buf, own, Sl, El, lk, accp, nll);
 #endif
   STAMP(wg, 2);
   const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
@@ -1229,18 +1271,20 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
   int u = w;
   V4 buf[kGroup];
   float cv[RP];
-  int wi = 0, j0 = 0, j1 = 0, k = 0;
+  int wi = 0, j0 = 0, j1 = 0, js = 1, k = 0;
   const V4* src = nullptr;
   const uint32_t lo = (uint32_t)lane * (uint32_t)sizeof(V4);
   auto unit_begin = [&](int uu) {
     const int ks = uu / NP, part = uu - ks * NP;
     wi = t * nks + ks;
     const int W4 = width[wi] >> 2;
-    j0 = part;  // strided parts: chunks part, part + NP, ...
-    j1 = W4;
+    const PartRange pr = part_range(W4, part, NP);
+    j0 = pr.j0;
+    j1 = pr.j1;
+    js = pr.js;
     src = reinterpret_cast<const V4*>(ent + off[wi]);
     QSC_DCHECK(off[wi] + (int64_t)width[wi] * 64 <= lk.dbg_ent[1]);
-    load_group(src, lo, 64, j0, NP, max(j1 - 1, 0), buf);
+    load_group(src, lo, 64, j0, js, max(j1 - 1, 0), buf);
     k = kmap[wi * 64 + lane];  // this lane's bin (count-sorted order)
     QSC_DCHECK(k >= 0 && k < Kp);
 #pragma unroll
@@ -1275,7 +1319,7 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, NP, buf, own, Sl, El, lk, accp, nll);
+    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, js, buf, own, Sl, El, lk, accp, nll);
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (NP == 1) {
       // the unit is the whole (tile, k-slice): its slab rows straight from registers
@@ -1614,68 +1658,92 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
     ++n;
     return more;
   };
-  // 3. C-pass units of the tile at the new S (cpass_tile_kernel steps 1, 3, 4)
+  // 3. C-pass units of the tile at the new S (cpass_tile_kernel steps 1, 3, 4).
+  //
+  // Phase split (c_split, qsc_obs_split; NP > 1, one C-pass unit per wave, >= 2 S-step rounds):
+  // the first S-step round updates tile rows [0, NW*QSC_SLICE), and every list's chunks j < m
+  // hold only such rows, so right after that round each wave walks its unit's chunks < m
+  // (phase A; the partial dC goes to the unit's part-sum slot in LDS, the NLL pair stays in
+  // registers) while the later rounds' slice reads are in flight, and after the last round the
+  // chunks >= m (phase B), continuing the same accumulators: the same sums in the same order as
+  // the unsplit walk, part of the C-pass arithmetic overlapping the S-step's HBM traffic.
+  const bool split =
+      QSC_PHASE_SPLIT && c_split != nullptr && NP > 1 && U <= NW && nsl >= 2 * NW && 2 * NP <= R;
   int u = w;
   V4 buf[kGroup];
   float cv[RP];
-  int wi = 0, j0 = 0, j1 = 0, k = 0;
+  int wi = 0, jb = 0, je = 0, js = 1, k = 0;
   const V4* src = nullptr;
   const uint32_t lo = (uint32_t)lane * (uint32_t)sizeof(V4);
-  auto unit_begin = [&](int uu) {
+  // unit uu: its list block, first chunk jb and end je of this walk (phase 0: whole list;
+  // 1: chunks < m; 2: chunks >= m), the read-ahead of its first chunk group, its bin and C
+  auto unit_begin = [&](int uu, int phase) {
     const int ks = uu / NP, part = uu - ks * NP;
     wi = t * nks + ks;
     const int W4 = c_width[wi] >> 2;
-    j0 = part;  // strided parts: chunks part, part + NP, ...
-    j1 = W4;
+    const int m = phase ? min(c_split[wi], W4) : 0;
+    const PartRange pr = part_range(W4, part, NP);
+    jb = pr.j0;
+    je = phase == 1 ? m : pr.j1;
+    js = pr.js;
+    if (phase == 2) jb = part + ((max(m - part, 0) + NP - 1) / NP) * NP;  // (strided parts)
     src = reinterpret_cast<const V4*>(c_ent + c_off[wi]);
     QSC_DCHECK(c_off[wi] + (int64_t)c_width[wi] * 64 <= lk.dbg_ent[1]);
-    load_group(src, lo, 64, j0, NP, max(j1 - 1, 0), buf);
+    load_group(src, lo, 64, jb, js, max(pr.j1 - 1, 0), buf);
     k = c_kmap[wi * 64 + lane];  // this lane's bin (count-sorted order)
     QSC_DCHECK(k >= 0 && k < Kp);
 #pragma unroll
     for (int r = 0; r < RP; ++r) cv[r] = Cl[min(k, K - 1) * CP + r];  // C_i, as the S-step used
   };
-  // Phase split (c_split, qsc_obs_split; one C-pass unit per wave and >= 2 S-step rounds): the
-  // first S-step round updates tile rows [0, NW*QSC_SLICE); every list's chunks j < m hold only
-  // such rows, so right after that round the unit walks its chunks < m (phase A) while the
-  // second round's slice reads are still in flight, and its chunks >= m after the last round
-  // (phase B), continuing the same accumulators: the same sums in the same order as the
-  // unsplit walk, with part of the C-pass arithmetic overlapping the S-step's HBM traffic.
-  const bool split = c_split != nullptr && U <= NW && nsl >= 2 * NW;
-  f2v sp_own[RP / 2], sp_acc[RP / 2], sp_nll = splat2(0.0f);
-  int sp_m = 0;
+  // the walk of the current unit from accumulators acc (zero, or phase A's partial in Pl)
+  f2v cnll = splat2(0.0f);
+  auto unit_walk = [&]<bool PFC = (QSC_ROW_PF_C != 0)>(bool from_pl, f2v (&accp)[RP / 2]) {
+    f2v own[RP / 2];
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j)
+      own[j] = f2v{(2 * j < R && k < K) ? cv[2 * j] : 0.0f,
+                   (2 * j + 1 < R && k < K) ? cv[2 * j + 1] : 0.0f} * splat2(own_scale);
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j)
+      accp[j] = from_pl ? f2v{2 * j < R ? Pl[((size_t)u * R + 2 * j) * 64 + lane] : 0.0f,
+                              2 * j + 1 < R ? Pl[((size_t)u * R + 2 * j + 1) * 64 + lane] : 0.0f}
+                        : splat2(0.0f);
+    walk_groups<RP, E, KIND, LOG, PFC>(src, lo, 64, jb, je, js, buf, own, Sl, El, lk, accp,
+                                       cnll);
+  };
+  auto to_pl = [&](const f2v (&accp)[RP / 2]) {
+#pragma unroll
+    for (int j = 0; j < RP / 2; ++j) {
+      if (2 * j < R) Pl[((size_t)u * R + 2 * j) * 64 + lane] = accp[j].x;
+      if (2 * j + 1 < R) Pl[((size_t)u * R + 2 * j + 1) * 64 + lane] = accp[j].y;
+    }
+  };
+
+  // 2. S-step over the wave's slices (next slice's reads in flight; the two register sets
+  //    alternate, as in spass_kernel); phase A after the first round when split
   if (il < nsl) {
     SliceIn<RP, E, ADAM> nxt;
-    bool go = true;
+    bool more = one_slice(cur, nxt);  // round 1
     if (split) {
-      go = one_slice(cur, nxt);  // round 1: rows [0, NW*QSC_SLICE); round 2's reads in flight
-      __syncthreads();
+      __syncthreads();  // the first round's rows are in LDS
       STAMP(wg, 15);
       if (u < U) {
-        unit_begin(u);
-        sp_m = c_split[wi];
-#pragma unroll
-        for (int j = 0; j < RP / 2; ++j) {
-          sp_own[j] = f2v{(2 * j < R && k < K) ? cv[2 * j] : 0.0f,
-                          (2 * j + 1 < R && k < K) ? cv[2 * j + 1] : 0.0f} * splat2(own_scale);
-          sp_acc[j] = splat2(0.0f);
-        }
-        walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, min(sp_m, j1), NP, buf, sp_own, Sl, El, lk,
-                                      sp_acc, sp_nll);
+        unit_begin(u, 1);
+        f2v accp[RP / 2];
+        unit_walk.template operator()<false>(false, accp);  // (the plain walk: registers)
+        to_pl(accp);
+        // the lane's NLL pair waits in this tile's dC slab rows (written only at the end of
+        // the launch, after phase B has read it back): no registers held across the rounds
+        reinterpret_cast<f2v*>(slab + (int64_t)t * R * Kp)[u * 64 + lane] = cnll;
+        cnll = splat2(0.0f);
       }
       STAMP(wg, 16);
-      if (go) {
-        for (;;) {
-          if (!one_slice(nxt, cur)) break;
-          if (!one_slice(cur, nxt)) break;
-        }
-      }
-    } else {
-      for (;;) {
-        if (!one_slice(cur, nxt)) break;
-        if (!one_slice(nxt, cur)) break;
-      }
     }
+    if (more)
+      for (;;) {
+        if (!one_slice(nxt, cur)) break;
+        if (!one_slice(cur, nxt)) break;
+      }
   }
 
   // the next launch's S-step scalars, by the oldest wave of block 0 (it has slack: its slices
@@ -1683,53 +1751,17 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
   if (blockIdx.x == 0 && threadIdx.x == 0) adam_cache_store(acache, ad, step_s + 2);
 
   STAMP(wg, 2);
-  if (split) {
-    // phase B: the unit's chunks >= m (the first of its stride at or past m)
-    int jB = j0;
-    if (u < U) {
-      jB = j0 + ((max(sp_m - j0, 0) + NP - 1) / NP) * NP;
-      load_group(src, lo, 64, jB, NP, max(j1 - 1, 0), buf);
-    }
-    __syncthreads();  // the whole S tile is in LDS
-    STAMP(wg, 3);
-    if (u < U) {
-      walk_groups<RP, E, KIND, LOG>(src, lo, 64, jB, j1, NP, buf, sp_own, Sl, El, lk, sp_acc,
-                                    sp_nll);
-      const float nll_w = wave_sum_dpp(sp_nll.x + sp_nll.y) * kLn2;
-      if (NP == 1) {
-#pragma unroll
-        for (int j = 0; j < RP / 2; ++j) {
-          if (2 * j < R) slab[((int64_t)t * R + 2 * j) * Kp + k] = sp_acc[j].x;
-          if (2 * j + 1 < R) slab[((int64_t)t * R + 2 * j + 1) * Kp + k] = sp_acc[j].y;
-        }
-        if (lane == 0) part_nll_c[wi] = nll_w;
-      } else {
-#pragma unroll
-        for (int j = 0; j < RP / 2; ++j) {
-          if (2 * j < R) Pl[((size_t)u * R + 2 * j) * 64 + lane] = sp_acc[j].x;
-          if (2 * j + 1 < R) Pl[((size_t)u * R + 2 * j + 1) * 64 + lane] = sp_acc[j].y;
-        }
-        if (lane == 0) Nl[u] = nll_w;
-      }
-    }
-    u = U;  // (the unsplit unit loop below has nothing left)
-  } else {
-    if (u < U) unit_begin(u);
-    __syncthreads();  // the whole S tile is in LDS
-    STAMP(wg, 3);
+  if (u < U) {
+    unit_begin(u, split ? 2 : 0);
+    if (split) cnll = reinterpret_cast<const f2v*>(slab + (int64_t)t * R * Kp)[u * 64 + lane];
   }
+  __syncthreads();  // the whole S tile is in LDS
+  STAMP(wg, 3);
   for (; u < U; u += NW) {
-    f2v own[RP / 2];
-#pragma unroll
-    for (int j = 0; j < RP / 2; ++j)
-      own[j] = f2v{(2 * j < R && k < K) ? cv[2 * j] : 0.0f,
-                   (2 * j + 1 < R && k < K) ? cv[2 * j + 1] : 0.0f} * splat2(own_scale);
     f2v accp[RP / 2];
-#pragma unroll
-    for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
-    f2v nll = splat2(0.0f);
-    walk_groups<RP, E, KIND, LOG>(src, lo, 64, j0, j1, NP, buf, own, Sl, El, lk, accp, nll);
-    const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
+    unit_walk(split, accp);
+    const float nll_w = wave_sum_dpp(cnll.x + cnll.y) * kLn2;
+    cnll = splat2(0.0f);
     if (NP == 1) {
 #pragma unroll
       for (int j = 0; j < RP / 2; ++j) {
@@ -1738,14 +1770,10 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
       }
       if (lane == 0) part_nll_c[wi] = nll_w;
     } else {
-#pragma unroll
-      for (int j = 0; j < RP / 2; ++j) {
-        if (2 * j < R) Pl[((size_t)u * R + 2 * j) * 64 + lane] = accp[j].x;
-        if (2 * j + 1 < R) Pl[((size_t)u * R + 2 * j + 1) * 64 + lane] = accp[j].y;
-      }
+      to_pl(accp);
       if (lane == 0) Nl[u] = nll_w;
     }
-    if (u + NW < U) unit_begin(u + NW);
+    if (u + NW < U) unit_begin(u + NW, 0);
   }
   STAMP(wg, 4);
   if (NP > 1) {
@@ -2471,10 +2499,12 @@ static unsigned scpass_threads(const qsc_obs_desc* d, int R) {
 }
 
 QSC_API int32_t qsc_scpass_split_rows(const qsc_obs_desc* d, int32_t R) {
-  if (!desc_ok(d) || R < 1 || R > QSC_MAX_R) return 0;
+  if (!QSC_PHASE_SPLIT || !desc_ok(d) || R < 1 || R > QSC_MAX_R) return 0;
   const int NW = (int)(scpass_threads(d, R) / 64), nsl = d->PT / QSC_SLICE;
   const int NP = cpass_parts(d, R, d->rowfmt == 1);
-  if (nsl < 2 * NW || d->nks * NP > NW) return 0;  // the split needs one unit per wave
+  // the split needs part sums in LDS (NP > 1), one C-pass unit per wave and room for the
+  // phase-A NLL pairs in the tile's slab rows (2 NP <= R)
+  if (nsl < 2 * NW || NP < 2 || d->nks * NP > NW || 2 * NP > R) return 0;
   return NW * QSC_SLICE;
 }
 

@@ -479,6 +479,8 @@ def test_phase_split_fused_launch_is_bitexact():
     from quantized_spectrum_cartography_amd.obs import Observations
     d = _random_case(56, 8, 128, 128, 256)
     o = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=8, tile=1024)
+    if o.split_rows == 0:
+        pytest.skip("library built without the phase split (QSC_PHASE_SPLIT=0, the default)")
     assert o.split_rows == 16 * 32 and int(o.c_split.min()) > 0
     kw = dict(S_init=d["S0"], C_init=d["C0"], max_iter=9)
     a = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], obs=o, **kw)
