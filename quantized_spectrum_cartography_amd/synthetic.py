@@ -47,12 +47,13 @@ def kslab_onebit_problem(I, J, K_local, R, rank, world, dist=None, f=0.1, seed=2
     S_true and S0 are common to all ranks (same seed); C_true / C0 columns, the noise and the
     mask are drawn per slab.  The quantizer (thr = mean of the slabs' medians, sigma from the
     global min/max) is agreed over `dist` so that all slabs share one probit model."""
-    g = torch.Generator().manual_seed(seed)
-    S_true = torch.rand(R, 1, I, J, generator=g)
-    S0 = 0.5 * torch.rand(R, 1, I, J, generator=g)
-    gl = torch.Generator().manual_seed(seed + 1000 + rank)
-    C_true = torch.rand(R, K_local, generator=gl)
-    C0 = 0.5 * torch.rand(R, K_local, generator=gl)
+    # drawn on the device: every rank builds its slab at once without the host's CPU share
+    g = torch.Generator(device=device).manual_seed(seed)
+    S_true = torch.rand(R, 1, I, J, generator=g, device=device)
+    S0 = 0.5 * torch.rand(R, 1, I, J, generator=g, device=device)
+    gl = torch.Generator(device=device).manual_seed(seed + 1000 + rank)
+    C_true = torch.rand(R, K_local, generator=gl, device=device)
+    C0 = 0.5 * torch.rand(R, K_local, generator=gl, device=device)
     T = _model.get_tensor(S_true.to(device), C_true.to(device))
     stats = torch.tensor([float(T.median()), -float(T.min()), float(T.max())], dtype=torch.float64,
                          device=device)
@@ -65,12 +66,12 @@ def kslab_onebit_problem(I, J, K_local, R, rank, world, dist=None, f=0.1, seed=2
     thr, tmin, tmax = float(stats[0]), -float(stats[1]), float(stats[2])
     sigma = (tmax - tmin) / 4
     b = torch.tensor([0.0, thr, tmax])
-    noise = torch.randn(T.shape, generator=gl)
+    noise = torch.randn(T.shape, generator=gl, device=device)
     Y = _model.quantize(T, sigma, b, noise=noise).unsqueeze(1)
     del noise
-    Wx = torch.bernoulli(torch.full((K_local, 1, I, J), f), generator=gl)
-    return dict(S_true=S_true, C_true=C_true, b=b, sigma=sigma, Y=Y, Wx=Wx, S0=S0, C0=C0,
-                log_model=False, offset=0.0, thr=thr, T_true=T)
+    Wx = torch.bernoulli(torch.full((K_local, 1, I, J), f, device=device), generator=gl)
+    return dict(S_true=S_true.cpu(), C_true=C_true.cpu(), b=b, sigma=sigma, Y=Y, Wx=Wx,
+                S0=S0.cpu(), C0=C0.cpu(), log_model=False, offset=0.0, thr=thr, T_true=T)
 
 
 def ijslab_onebit_problem(I, J, K, R, rank, world, dist=None, f=0.1, seed=20260,
@@ -80,12 +81,12 @@ def ijslab_onebit_problem(I, J, K, R, rank, world, dist=None, f=0.1, seed=20260,
     C_true and C0 are common to all ranks (same seed); S_true / S0, the noise and the mask are
     drawn per block.  The quantizer (thr = mean of the blocks' medians, sigma from the global
     min/max) is agreed over `dist` so that all blocks share one probit model."""
-    g = torch.Generator().manual_seed(seed)
-    C_true = torch.rand(R, K, generator=g)
-    C0 = 0.5 * torch.rand(R, K, generator=g)
-    gl = torch.Generator().manual_seed(seed + 2000 + rank)
-    S_true = torch.rand(R, 1, I, J, generator=gl)
-    S0 = 0.5 * torch.rand(R, 1, I, J, generator=gl)
+    g = torch.Generator(device=device).manual_seed(seed)  # (on the device, as kslab_*)
+    C_true = torch.rand(R, K, generator=g, device=device)
+    C0 = 0.5 * torch.rand(R, K, generator=g, device=device)
+    gl = torch.Generator(device=device).manual_seed(seed + 2000 + rank)
+    S_true = torch.rand(R, 1, I, J, generator=gl, device=device)
+    S0 = 0.5 * torch.rand(R, 1, I, J, generator=gl, device=device)
     T = _model.get_tensor(S_true.to(device), C_true.to(device))
     stats = torch.tensor([float(T.median()), -float(T.min()), float(T.max())], dtype=torch.float64,
                          device=device)
@@ -98,12 +99,12 @@ def ijslab_onebit_problem(I, J, K, R, rank, world, dist=None, f=0.1, seed=20260,
     thr, tmin, tmax = float(stats[0]), -float(stats[1]), float(stats[2])
     sigma = (tmax - tmin) / 4
     b = torch.tensor([0.0, thr, tmax])
-    noise = torch.randn(T.shape, generator=gl)
+    noise = torch.randn(T.shape, generator=gl, device=device)
     Y = _model.quantize(T, sigma, b, noise=noise).unsqueeze(1)
     del noise
-    Wx = torch.bernoulli(torch.full((K, 1, I, J), f), generator=gl)
-    return dict(S_true=S_true, C_true=C_true, b=b, sigma=sigma, Y=Y, Wx=Wx, S0=S0, C0=C0,
-                log_model=False, offset=0.0, thr=thr, T_true=T)
+    Wx = torch.bernoulli(torch.full((K, 1, I, J), f, device=device), generator=gl)
+    return dict(S_true=S_true.cpu(), C_true=C_true.cpu(), b=b, sigma=sigma, Y=Y, Wx=Wx,
+                S0=S0.cpu(), C0=C0.cpu(), log_model=False, offset=0.0, thr=thr, T_true=T)
 
 
 def split_problem(prob, rank, world, shard):

@@ -115,3 +115,15 @@ def test_integration_stub_struct_matches_c():
     size, loss_off = _c_sizeof_model()
     assert ctypes.sizeof(ns["_Model"]) == size
     assert ns["_Model"].loss.offset == loss_off
+
+
+def test_integration_stub_error_path(libpath):
+    """The stub's error path turns a return code into its message:
+    exec the snippet's qsc_error_string declarations against the built library."""
+    import re
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    decl = "\n".join(re.findall(r"^_L\.qsc_error_string\..*$", text, re.M))
+    assert "restype = ctypes.c_char_p" in decl
+    ns = {"ctypes": ctypes, "_L": ctypes.CDLL(libpath)}
+    exec(decl, ns)
+    assert ns["_L"].qsc_error_string(_lib.QSC_EINVAL).decode() == "invalid argument"

@@ -67,3 +67,22 @@ def test_graph_chunks_cover_the_run(steps):
     from quantized_spectrum_cartography_amd import qmc
     ch = qmc.graph_chunks(steps // 2)
     assert sum(ch) == steps // 2 and max(ch) <= qmc.GRAPH_MAX_ITERS
+
+
+def test_ranks_share_the_cpu_threads(monkeypatch):
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(64)), raising=False)
+    assert bench.rank_env({"OMP_NUM_THREADS": "16"}, 8)["OMP_NUM_THREADS"] == "2"
+    assert bench.rank_env({}, 8)["OMP_NUM_THREADS"] == "8"
+    assert bench.rank_env({"OMP_NUM_THREADS": "4"}, 8)["OMP_NUM_THREADS"] == "1"
+    assert bench.rank_env({"X": "y"}, 2)["X"] == "y"
+
+
+def test_heartbeat_reports_long_phases(capsys):
+    import time
+    with bench.heartbeat(0, "phase", every=0.05):
+        time.sleep(0.2)
+    err = capsys.readouterr().err
+    assert "[bench] phase:" in err
+    with bench.heartbeat(1, "phase", every=0.05):  # other ranks stay quiet
+        time.sleep(0.12)
+    assert capsys.readouterr().err == ""

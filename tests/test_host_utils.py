@@ -47,3 +47,14 @@ def test_log_quantize_rejects_nonpositive_offset():
     for off in (0.0, -1e-3):
         with pytest.raises(ValueError):
             quantize(X, 1.0, b, offset=off, log_model=True, noise=torch.zeros(X.shape))
+
+
+def test_every_package_module_imports():
+    """Import-level check of every module of the package (no GPU needed to import)."""
+    import importlib
+    import pkgutil
+    import quantized_spectrum_cartography_amd as pkg
+    for m in pkgutil.iter_modules(pkg.__path__):
+        if m.name.startswith("libqsc"):  # (the HIP libraries, loaded through ctypes)
+            continue
+        importlib.import_module("%s.%s" % (pkg.__name__, m.name))

@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--warm-width", type=float, default=8.0)
     ap.add_argument("--warm-lr-s", type=float, default=1e-3)
     ap.add_argument("--prefit-steps", type=int, default=300)
+    ap.add_argument("--free-lr-scales", type=float, nargs="*", default=[1e-3, 1e-4])
+    ap.add_argument("--skip-c2", action="store_true")
     args = ap.parse_args()
     from quantized_spectrum_cartography_amd import dip, maps, metrics, qmc, synthetic
     from quantized_spectrum_cartography_amd import quantization_model_log as qml
@@ -50,7 +52,7 @@ def main():
 
     # ---- C2 free S, BASELINE recipe (f = 0.1) and the same map sampled at f = 0.5 ----
     I, J, K, R = synthetic.CONFIGS["c2"]
-    for name, f in (("c2_free_s", 0.1), ("c2_free_s_f05", 0.5)):
+    for name, f in (() if args.skip_c2 else (("c2_free_s", 0.1), ("c2_free_s_f05", 0.5))):
         p = synthetic.onebit_problem(I, J, K, R, f=f, seed=20262)
         marks = sorted({int(round(x / 10.0)) * 10 for x in np.geomspace(10, args.c2_iters, 14)})
         t0 = time.perf_counter()
@@ -159,6 +161,28 @@ def c5_warm_runs(Y, Wx, b, T, S_true, R, args):
                           "wall_s": time.perf_counter() - t0,
                           "cost_first": rd.costs_s[0], "cost_last": rd.costs_s[-1]}
     print(json.dumps({"c5_dip_warm": [lin_f, lg_f]}), file=sys.stderr, flush=True)
+    # free S from the warm start (qmc.solve, log model), Adam steps scaled to the warm-start
+    # fields (lr = scale x mean |S0| / mean |C0|), map NMSE every 10 iterations on the device
+    from quantized_spectrum_cartography_amd import qmc
+    s_mag, c_mag = float(S0.abs().mean()), float(C0.abs().mean())
+    for scale in args.free_lr_scales:
+        t0 = time.perf_counter()
+        rf = qmc.solve(Y, Wx, b, 5.0, R, S_init=S0.cpu(), C_init=C0.cpu(), offset=LOG_OFFSET_4,
+                       log_model=True, lr_s=scale * s_mag, lr_c=scale * c_mag,
+                       max_iter=args.warm_iters, use_graph=True, T_true=T, nmse_every=10)
+        torch.cuda.synchronize()
+        tr = [[10 * (i + 1), round(float(v), 5)] for i, v in enumerate(rf.nmse)]
+        lin_f, lg_f = _nmse_pair(rf.S, rf.C, T, LOG_OFFSET_4)
+        out["c5_free_warm_lr%g" % scale] = {
+            "iters": args.warm_iters, "lr_s": scale * s_mag, "lr_c": scale * c_mag,
+            "map_nmse": tr[:: max(1, len(tr) // 12)], "map_nmse_best": min(tr, key=lambda x: x[1]),
+            "map_nmse_final": lin_f, "map_nmse_log_final": lg_f,
+            "slf_nmse": (metrics.slf_nmse(rf.S, S_true) if bool(torch.isfinite(rf.S).all())
+                         else None),  # (free S can leave T_hat + offset <= 0: log of it NaN)
+            "wall_s": time.perf_counter() - t0,
+            "cost_first": rf.costs_s[0], "cost_last": rf.costs_s[-1]}
+        print(json.dumps({"c5_free_warm_lr%g" % scale: [lin_f, lg_f]}), file=sys.stderr,
+              flush=True)
     return out
 
 
