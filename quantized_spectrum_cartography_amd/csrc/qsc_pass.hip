@@ -1404,16 +1404,89 @@ struct FusedBlock {
   static constexpr int v = RP > 8 ? 512 : 64 * QSC_FUSED_WAVES;
 };
 
+// (device-function form: the 2 KB edge table by reference; kernel form below: by value --
+// a kernel argument is never a reference, which would hand the device a host address)
+#define QSC_SCF_PARAMS                                                                         \
+  const E *__restrict__ s_ent, const int *__restrict__ s_width, const int64_t *__restrict__ s_off, \
+      const E *__restrict__ c_ent, const int *__restrict__ c_width,                                \
+      const int64_t *__restrict__ c_off, const int *__restrict__ c_kmap, int nks, int NP, int PT,  \
+      Lik lk, const Edges &E_, int nbins, int R, int K, float *__restrict__ S,                    \
+      const float *__restrict__ C,                                                                \
+      float *__restrict__ mS, float *__restrict__ vS, qsc_adam ad, float lambda_s,                \
+      qsc_state *__restrict__ st, float *__restrict__ part_nll_s, float *__restrict__ part_nsq_s, \
+      float *__restrict__ slab, float *__restrict__ part_nll_c, float *__restrict__ cnsq,         \
+      AdamCache *__restrict__ acache, const int *__restrict__ c_split
+#define QSC_SCF_KPARAMS                                                                        \
+  const E *__restrict__ s_ent, const int *__restrict__ s_width, const int64_t *__restrict__ s_off, \
+      const E *__restrict__ c_ent, const int *__restrict__ c_width,                                \
+      const int64_t *__restrict__ c_off, const int *__restrict__ c_kmap, int nks, int NP, int PT,  \
+      Lik lk, Edges E_, int nbins, int R, int K, float *__restrict__ S,                           \
+      const float *__restrict__ C,                                                                \
+      float *__restrict__ mS, float *__restrict__ vS, qsc_adam ad, float lambda_s,                \
+      qsc_state *__restrict__ st, float *__restrict__ part_nll_s, float *__restrict__ part_nsq_s, \
+      float *__restrict__ slab, float *__restrict__ part_nll_c, float *__restrict__ cnsq,         \
+      AdamCache *__restrict__ acache, const int *__restrict__ c_split
+#define QSC_SCF_ARGS                                                                            \
+  s_ent, s_width, s_off, c_ent, c_width, c_off, c_kmap, nks, NP, PT, lk, E_, nbins, R, K, S, C, mS, \
+      vS, ad, lambda_s, st, part_nll_s, part_nsq_s, slab, part_nll_c, cnsq, acache, c_split
+
+// the fused launch's operands as one struct (scloop_kernel reads them through the kernel
+// argument segment every iteration)
+template <typename E>
+struct ScfArgs {
+  const E* s_ent;
+  const int* s_width;
+  const int64_t* s_off;
+  const E* c_ent;
+  const int* c_width;
+  const int64_t* c_off;
+  const int* c_kmap;
+  int nks, NP, PT;
+  Lik lk;
+  Edges E_;
+  int nbins, R, K;
+  float* S;
+  const float* C;
+  float *mS, *vS;
+  qsc_adam ad;
+  float lambda_s;
+  qsc_state* st;
+  float *part_nll_s, *part_nsq_s, *slab, *part_nll_c, *cnsq;
+  AdamCache* acache;
+  const int* c_split;
+  // the C-finish half (scloop_kernel)
+  float *Cw, *mC, *vC;
+  qsc_adam adc;
+  float lambda_c;
+  float* hist;
+  int hist_cap;
+  AdamCache* acache_c;
+  int niter;
+  unsigned* bar;
+};
+// a by-value copy of a struct held in the kernel argument segment (scalar loads)
+template <typename T>
+__device__ __forceinline__ T ld_arg(const T __attribute__((address_space(4))) & x) {
+  static_assert(sizeof(T) % 4 == 0, "argument structs are whole dwords");
+  T out;
+  const uint32_t __attribute__((address_space(4)))* src =
+      (const uint32_t __attribute__((address_space(4)))*)&x;
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&out);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = src[i];
+  return out;
+}
+#define QSC_SCF_ARGS_OF(a)                                                                     \
+  a.s_ent, a.s_width, a.s_off, a.c_ent, a.c_width, a.c_off, a.c_kmap, a.nks, a.NP, a.PT,        \
+      ld_arg<Lik>(a.lk), *(const Edges*)(&a.E_), a.nbins, a.R, a.K, a.S, a.C, a.mS, a.vS,       \
+      ld_arg<qsc_adam>(a.ad), a.lambda_s, a.st, a.part_nll_s, a.part_nsq_s, a.slab,              \
+      a.part_nll_c, a.cnsq, a.acache, a.c_split
+
+// One pixel tile t of nt of the fused launch (scfused_kernel: t = the workgroup; scloop_kernel:
+// the same tile every iteration; C is read-only within a call -- the loop kernel's C-finish
+// writes it between calls, behind grid barriers).
 template <int RP, typename E, int KIND, bool LOG>
-__global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
-    const E* __restrict__ s_ent, const int* __restrict__ s_width, const int64_t* __restrict__ s_off,
-    const E* __restrict__ c_ent, const int* __restrict__ c_width, const int64_t* __restrict__ c_off,
-    const int* __restrict__ c_kmap, int nks, int NP, int PT, Lik lk, Edges E_, int nbins, int R,
-    int K, float* __restrict__ S,
-    const float* __restrict__ C, float* __restrict__ mS, float* __restrict__ vS, qsc_adam ad,
-    float lambda_s, qsc_state* __restrict__ st, float* __restrict__ part_nll_s,
-    float* __restrict__ part_nsq_s, float* __restrict__ slab, float* __restrict__ part_nll_c,
-    float* __restrict__ cnsq, AdamCache* __restrict__ acache, const int* __restrict__ c_split) {
+__device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const int nt) {
   using V4 = typename Ent<E>::V4;
   constexpr int CP = TP<RP, KIND>::v;  // C^T row pitch == S tile row pitch
   constexpr int RH = RP / 2;
@@ -1428,7 +1501,6 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
   const int NW = blockDim.x >> 6;
   const int U = nks * NP;
   float* Nl = Pl + (NP > 1 ? (size_t)U * R * 64 : 0);               // [max(U,16)]
-  const int t = blockIdx.x, nt = gridDim.x;
   const int Kp = nks * 64;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int p = lane & (QSC_SLICE - 1), h = lane >> 5;
@@ -1437,7 +1509,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
   // this wave's n-th slice of the tile (local index) and its global slice
   auto local_of = [&](int n) { return n * NW + ((n & 1) ? (NW - 1 - w) : w); };
   auto global_of = [&](int i) { return i * nt + ((i & 1) ? (nt - 1 - t) : t); };
-  [[maybe_unused]] const int wg = blockIdx.x * (FusedBlock<RP>::v / 64) + w;  // (stamps)
+  [[maybe_unused]] const int wg = t * (FusedBlock<RP>::v / 64) + w;  // (stamps)
   STAMP(wg, 0);
   RSTAMP(wg, 28);
 #if QSC_DIAG_STAMPS
@@ -1557,7 +1629,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
       const float nrm = sqrtf(nsq_s);
       sc.coef = nrm > 0.0f ? lambda_s / nrm : 0.0f;
       sc.as = adam_scalars_cached(((step_s + 1) & 1) ? ac1 : ac0, ad, step_s + 1);
-      if (blockIdx.x == 0) {
+      if (t == 0) {
         // book-keeping of spass_kernel (mode 1)
         int pend = st->pending;
         if (pend & QSC_PEND_C) st->step_c += 1;
@@ -1578,7 +1650,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
   __syncthreads();
   if (!early) slice_load(cur, s_ent, s_width, s_off, global_of(il < nsl ? il : 0), ln, S, mS, vS);
   STAMP(wg, 1);
-  if (blockIdx.x == 0) {
+  if (t == 0) {
     // ||C_i||^2 for the next C update's regulariser, from the staged C^T at the start (as a
     // chain of dependent global reads at the end it delayed the last workgroup); the order of
     // cnorm_sq: thread t < 256 accumulates flat indices t, t + 256, ..., then block_sum
@@ -1748,7 +1820,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
 
   // the next launch's S-step scalars, by the oldest wave of block 0 (it has slack: its slices
   // are done long before the tile barrier)
-  if (blockIdx.x == 0 && threadIdx.x == 0) adam_cache_store(acache, ad, step_s + 2);
+  if (t == 0 && threadIdx.x == 0) adam_cache_store(acache, ad, step_s + 2);
 
   STAMP(wg, 2);
   if (u < U) {
@@ -1801,6 +1873,11 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(
   RSTAMP(wg, 29);
 }
 
+template <int RP, typename E, int KIND, bool LOG>
+__global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(QSC_SCF_KPARAMS) {
+  scfused_tile<RP, E, KIND, LOG>(QSC_SCF_ARGS, (int)blockIdx.x, (int)gridDim.x);
+}
+
 // LDS bytes of scfused_kernel
 size_t scfused_lds(int PT, int R, int K, int nks, int NP, bool sr) {
   const size_t U = (size_t)nks * NP;
@@ -1844,17 +1921,23 @@ __device__ void settle_s(qsc_state* __restrict__ st, const float* __restrict__ p
 // ---------------------------------------------------------------------------------------
 // C finish: fixed-order slab reduction (+ fused regulariser / Adam / projection)
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(kFBlock) cfinish_kernel(
-    const float* __restrict__ slab, int ntiles, int nks, int R, int K, float* __restrict__ C,
-    int mode, float* __restrict__ dC, float* __restrict__ mC, float* __restrict__ vC,
-    qsc_adam ad, float lambda_c, const float* __restrict__ normsq_ext,
-    const float* __restrict__ cnsq, qsc_state* __restrict__ st,
-    const float* __restrict__ part_nll_c, int npart_c, const float* __restrict__ part_nll_s,
-    const float* __restrict__ part_nsq_s, int nslices, float* __restrict__ hist, int hist_cap,
-    AdamCache* __restrict__ acache) {
-  constexpr int NW = kFBlock / 64;
-  __shared__ float red[NW][64];
-  __shared__ Scalars sc;
+#define QSC_CF_PARAMS                                                                          \
+  const float *__restrict__ slab, int ntiles, int nks, int R, int K, float *C, int mode,         \
+      float *__restrict__ dC, float *__restrict__ mC, float *__restrict__ vC, qsc_adam ad,       \
+      float lambda_c, const float *__restrict__ normsq_ext, const float *__restrict__ cnsq,      \
+      qsc_state *__restrict__ st, const float *__restrict__ part_nll_c, int npart_c,             \
+      const float *__restrict__ part_nll_s, const float *__restrict__ part_nsq_s, int nslices,   \
+      float *__restrict__ hist, int hist_cap, AdamCache *__restrict__ acache
+#define QSC_CF_ARGS                                                                           \
+  slab, ntiles, nks, R, K, C, mode, dC, mC, vC, ad, lambda_c, normsq_ext, cnsq, st, part_nll_c,  \
+      npart_c, part_nll_s, part_nsq_s, nslices, hist, hist_cap, acache
+constexpr int kFWaves = kFBlock / 64;
+
+// C-finish work item vb of R*nks + 2 (cfinish_kernel: vb = the workgroup; scloop_kernel: the
+// workgroups' share of them after a grid barrier), with its LDS scratch passed in
+__device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scalars& sc,
+                                           float (*sh3)[kFWaves], QSC_CF_PARAMS) {
+  constexpr int NW = kFWaves;
   const int Kp = nks * 64;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 
@@ -1862,17 +1945,16 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
   // or the caller's global value (K-slab); never re-read here, where blocks overwrite C
   const float nsq = normsq_ext ? *normsq_ext : *cnsq;
 
-  if (blockIdx.x == R * nks + 1) {
+  if (vb == R * nks + 1) {
     // the next C-step's Adam scalars (the next S-pass settles step_c + 1 in between)
     if (mode == 1 && threadIdx.x == 0) adam_cache_store(acache, ad, st->step_c + 2);
     return;
   }
-  if (blockIdx.x == R * nks) {
+  if (vb == R * nks) {
     // book-keeping block: settle the S-pass partials (settle_s) and total the C-pass NLL.
     // Every partial is read up front (one memory round trip, batches of 8 loads in flight)
     // and the three fixed-order block sums share one LDS pass; same sums, same order as
     // settle_s + block_sum.
-    __shared__ float sh3[3][NW];
     const int pend = st->pending;
     const bool settle = (pend & (QSC_PEND_SNLL | QSC_PEND_SUPD)) != 0;
     const bool supd = (pend & QSC_PEND_SUPD) != 0;
@@ -1935,7 +2017,7 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
     return;
   }
 
-  const int r = blockIdx.x / nks, ks = blockIdx.x - r * nks;
+  const int r = vb / nks, ks = vb - r * nks;
   const int k = ks * 64 + lane;
   // wave 0 reads its C / moments ahead of the tile sum (one HBM round trip instead of two)
   float p0 = 0.0f, m0 = 0.0f, v0 = 0.0f;
@@ -1987,6 +2069,96 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(
   }
 }
 
+__global__ void __launch_bounds__(kFBlock) cfinish_kernel(QSC_CF_PARAMS) {
+  __shared__ float red[kFWaves][64];
+  __shared__ Scalars sc;
+  __shared__ float sh3[3][kFWaves];
+  cfinish_vb((int)blockIdx.x, red, sc, sh3, QSC_CF_ARGS);
+}
+
+// ---------------------------------------------------------------------------------------
+// Persistent fused loop: n outer iterations of (scpass, cfinish) in one launch
+// ---------------------------------------------------------------------------------------
+// The workgroup of tile t keeps that tile for every iteration: S-step i + C-pass i+1 of the
+// tile (scfused_tile), grid barrier, its share of the C-finish work items (cfinish_vb), grid
+// barrier.  Same code, same operands, same order as the launch pair, so the results are those
+// of (qsc_scpass, qsc_cfinish) x n bit for bit; what goes is the pair's launch ramps and the
+// C-finish's own dispatch.  qsc_scloop launches it only when every workgroup is resident at
+// once (one per CU at C3), which the barriers need.
+//
+// Grid barrier: every thread makes its writes visible device-wide (agent-scope fence), the
+// workgroup meets, one thread adds its arrival to the launch's counter (device-scope atomic)
+// and polls it (acquire loads) until `target`; the workgroup then meets again behind an
+// agent-scope fence.  A wait longer than kLoopSpin polls (a grid that is not all resident)
+// raises the sticky loop_fault word of the state and every workgroup leaves the launch at its
+// next barrier, so the grid always drains; the host reports the fault (read_state).
+constexpr unsigned kLoopSpin = 1u << 20;
+
+__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, int* fault, int* okl) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned polls = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+        ok = 0;
+        break;
+      }
+      if (++polls > kLoopSpin) {
+        __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    *okl = ok;
+  }
+  __syncthreads();
+  const bool ok = *okl != 0;
+  __threadfence();
+  return ok;
+}
+
+template <int RP, typename E, int KIND, bool LOG>
+__global__ void __launch_bounds__(FusedBlock<RP>::v) scloop_kernel(const ScfArgs<E> args) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  using KArgs = const ScfArgs<E> __attribute__((address_space(4)));
+  const int t = blockIdx.x, nt = gridDim.x;
+  // C-finish scratch and the barrier's broadcast word, over the (then idle) tile LDS
+  float(*red)[64] = reinterpret_cast<float(*)[64]>(smem);
+  float(*sh3)[kFWaves] = reinterpret_cast<float(*)[kFWaves]>(smem + kFWaves * 64);
+  Scalars& sc = *reinterpret_cast<Scalars*>(smem + kFWaves * 64 + 3 * kFWaves);
+  int* okl = reinterpret_cast<int*>(smem + kFWaves * 64 + 3 * kFWaves + 16);
+  unsigned target = 0;
+  for (int it = 0; it < args.niter; ++it) {
+    // the operands are re-read from the argument segment each iteration (an opaque pointer to
+    // it): held across iterations they would need more scalar registers than there are
+    KArgs* ap = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(ap));
+    scfused_tile<RP, E, KIND, LOG>(QSC_SCF_ARGS_OF((*ap)), t, nt);
+    // (a second opaque pointer: the C-finish half re-reads what it needs instead of keeping
+    // the tile half's operands live through the whole tile)
+    KArgs* bp = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(bp));
+    KArgs& a = *bp;
+    int* fault = reinterpret_cast<int*>(a.st) + 9;  // qsc_state.loop_fault
+    target += (unsigned)nt;
+    if (!grid_sync(a.bar, target, fault, okl)) return;
+    for (int vb = t; vb < a.R * a.nks + 2; vb += nt) {
+      cfinish_vb(vb, red, sc, sh3, a.slab, nt, a.nks, a.R, a.K, a.Cw, 1, nullptr, a.mC, a.vC,
+                 ld_arg<qsc_adam>(a.adc), a.lambda_c, nullptr, a.cnsq, a.st, a.part_nll_c, nt * a.nks,
+                 a.part_nll_s, a.part_nsq_s, nt * a.PT / QSC_SLICE, a.hist, a.hist_cap,
+                 a.acache_c);
+      __syncthreads();
+    }
+    target += (unsigned)nt;
+    if (!grid_sync(a.bar, target, fault, okl)) return;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // C update from an externally reduced gradient g [R][K] (IJ-slab sharding, after the RCCL
 // all-reduce of the per-shard dC): g + lambda_c C/||C||, Adam, C >= 0; the same state
 // protocol as qsc_cfinish mode 1.  normsq_s_ext (nullable): the all-reduced ||S||^2, stored as
@@ -2174,6 +2346,7 @@ struct PassWs {
   int* sched;       // S-pass queue counters [kSchedQ] + finished-wave counter (zero between launches)
   float* cnsq;      // ||C||^2 of the C the last C-pass read (written by the C-pass)
   AdamCache* acache;  // [0..1] S-side, [2..3] C-side step scalars (adam_scalars_cached)
+  unsigned* bar;      // scloop_kernel's grid-barrier arrivals (zeroed before each launch)
 };
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -2197,6 +2370,8 @@ PassWs carve(const qsc_obs_desc* d, int R, void* ws) {
   p.cnsq = (float*)w;
   w += al(4);
   p.acache = (AdamCache*)w;
+  w += al(4 * sizeof(AdamCache));
+  p.bar = (unsigned*)w;
   return p;
 }
 
@@ -2204,7 +2379,7 @@ size_t ws_bytes_for(const qsc_obs_desc* d, int R) {
   const int64_t Kp = (int64_t)d->nks * 64;
   return al((size_t)d->ntiles * R * Kp * 4) + al((size_t)d->ntiles * d->nks * 4) +
          2 * al((size_t)(d->Pp / QSC_SLICE) * 4) + al(256 * 8) + al((kSchedQ + 1) * 4) + al(4) +
-         al(4 * sizeof(AdamCache));
+         al(4 * sizeof(AdamCache)) + al(4);
 }
 
 bool desc_ok(const qsc_obs_desc* d) {
@@ -2291,6 +2466,40 @@ int spass_bpc(int RP) { return RP > 8 ? 2 : RP == 8 ? QSC_SPASS_BPC8 : QSC_SPASS
   } while (0)
 
 static bool rowfmt_ok(const qsc_obs_desc* d, int R, int kind);
+static unsigned scpass_threads(const qsc_obs_desc* d, int R);
+static int cpass_parts(const qsc_obs_desc* d, int R, bool sr);
+
+// one scloop_kernel launch (rank <= 8: 16-wave workgroups, the C-finish's width), after
+// checking that the whole grid is resident at once
+template <int RPV, typename ET, int KD, bool LG>
+static int scloop_launch(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
+                         const int64_t* s_off, const void* c_entries, const int32_t* c_width,
+                         const int64_t* c_off, const int32_t* c_kmap, int NP, const Lik& lk,
+                         const Edges& E, int R, float* S, float* C, float* mS, float* vS,
+                         const qsc_adam& ad, float lambda_s, float* mC, float* vC,
+                         const qsc_adam& adc, float lambda_c, qsc_state* st, float* hist,
+                         int hist_cap, int niter, const PassWs& w, unsigned threads, size_t shm,
+                         hipStream_t s) {
+  if constexpr (RPV > 8) {
+    return QSC_EINVAL;
+  } else {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &nb, reinterpret_cast<const void*>(&scloop_kernel<RPV, ET, KD, LG>), (int)threads,
+            shm) != hipSuccess ||
+        (int64_t)nb * cu_count() < d->ntiles)
+      return QSC_EINVAL;
+    QSC_TRY(hipMemsetAsync(w.bar, 0, sizeof(unsigned), s));
+    ScfArgs<ET> a{(const ET*)s_entries, s_width, s_off, (const ET*)c_entries, c_width, c_off,
+                  c_kmap, d->nks, NP, d->PT, lk, E, d->nbins, R, d->K, S, C, mS, vS, ad,
+                  lambda_s, st, w.snll, w.snsq, w.slab, w.cnll, w.cnsq, w.acache, nullptr, C,
+                  mC, vC, adc, lambda_c, hist, hist_cap, w.acache + 2, niter, w.bar};
+    hipLaunchKernelGGL((scloop_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles), dim3(threads),
+                       shm, s, a);
+    QSC_CHECK_LAUNCH();
+    return QSC_OK;
+  }
+}
 
 extern "C" {
 
@@ -2553,6 +2762,53 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
 #undef SCPASS_LAUNCH
   QSC_CHECK_LAUNCH();
   return QSC_OK;
+}
+
+QSC_API int qsc_scloop_supported(const qsc_obs_desc* d, int32_t R) {
+  if (!qsc_scpass_supported(d, R) || rp_of(R) > 8) return 0;
+  return (scpass_threads(d, R) == (unsigned)kFBlock && d->ntiles <= cu_count()) ? 1 : 0;
+}
+
+QSC_API int qsc_scloop(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
+                       const int64_t* s_off, const void* c_entries, const int32_t* c_width,
+                       const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m, int32_t R,
+                       float* S, float* C, float* mS, float* vS, const qsc_adam* adam_s,
+                       float lambda_s, float* mC, float* vC, const qsc_adam* adam_c,
+                       float lambda_c, qsc_state* st, float* hist, int32_t hist_cap,
+                       int32_t niter, void* ws, size_t ws_bytes, void* stream) {
+  if (!qsc_scloop_supported(d, R) || !m || m->nbounds - 1 != d->nbins || !S || !C || !mS ||
+      !vS || !adam_s || !mC || !vC || !adam_c || !st || !s_width || !s_off || !c_width ||
+      !c_off || !c_kmap || (d->s_entries > 0 && !s_entries) ||
+      (d->c_entries > 0 && !c_entries) || !ws || ws_bytes < ws_bytes_for(d, R) || niter < 0 ||
+      (hist_cap > 0 && !hist))
+    return QSC_EINVAL;
+  if (niter == 0) return QSC_OK;
+  const int RP = rp_of(R);
+  const int kind = lik_kind(m);
+  const bool sr = d->rowfmt == 1;
+  if (!rowfmt_ok(d, R, kind)) return QSC_EINVAL;
+  const int NP = cpass_parts(d, R, sr);
+  const size_t shm = scfused_lds(d->PT, R, d->K, d->nks, NP, sr);
+  PassWs w = carve(d, R, ws);
+  Edges E;
+  make_edges(m, &E);
+  Lik lk = make_lik(m);
+  set_dbg(lk, d, sr);
+  if (kind == LIK_SQUARED)
+    make_sq_targets(m, &E);
+  else if (!m->log_model)
+    scale_edges(&E, m->nbounds - 1, lk.a);
+  const unsigned threads = scpass_threads(d, R);
+  hipStream_t s = STREAM(stream);
+  int rc = QSC_EINVAL;
+#define SCLOOP_LAUNCH(RPV, ET, KD, LG)                                                         \
+  rc = scloop_launch<RPV, ET, KD, LG>(d, s_entries, s_width, s_off, c_entries, c_width, c_off,  \
+                                      c_kmap, NP, lk, E, R, S, C, mS, vS, *adam_s, lambda_s,   \
+                                      mC, vC, *adam_c, lambda_c, st, hist, hist_cap, niter, w,  \
+                                      threads, shm, s)
+  QSC_DISPATCH_PASS(SCLOOP_LAUNCH);
+#undef SCLOOP_LAUNCH
+  return rc;
 }
 
 QSC_API int qsc_cfinish(const qsc_obs_desc* d, int32_t R, float* C, int32_t mode, float* dC,

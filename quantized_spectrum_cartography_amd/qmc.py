@@ -14,6 +14,7 @@ loop at :559-645); qmc/qmc.py is only its import preamble.  Per outer iteration 
     reference's GAN path, Z optimised, network frozen: :547-550).
 """
 import math
+import os
 import warnings
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -37,6 +38,7 @@ class SolveResult:
     Z: Optional[torch.Tensor] = None
     iters: int = 0
     fused: bool = False                 # S-step + next C-pass ran as one launch (qsc_scpass)
+    looped: bool = False                # the fused bodies ran as one persistent launch (qsc_scloop)
 
 
 # Longest run captured as one hipGraph; longer runs replay several (results are identical:
@@ -50,8 +52,11 @@ def issue_iterations(solver, n):
     finish): c_step, fused_body x (n-1), s_step -- two launches per iteration."""
     if getattr(solver, "fuse", False) and n >= 2:
         solver.c_step()
-        for _ in range(n - 1):
-            solver.fused_body()
+        if getattr(solver, "loop", False):
+            solver.fused_loop(n - 1)  # the n-1 bodies as one persistent launch (qsc_scloop)
+        else:
+            for _ in range(n - 1):
+                solver.fused_body()
         solver.s_step()
     else:
         for _ in range(n):
@@ -210,7 +215,7 @@ class FreeSSolver:
 
     def __init__(self, obs, S_init, C_init, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
                  betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024, fuse=True,
-                 T_true=None, nmse_every=0):
+                 T_true=None, nmse_every=0, loop=True):
         self.obs = obs
         R = S_init.shape[0]
         self.R = R
@@ -236,6 +241,11 @@ class FreeSSolver:
                                           dtype=torch.float64, device=self.S.device)
             self._nmse_ws = torch.empty(_lib.lib().qsc_reduce_workspace_bytes(0),
                                         dtype=torch.uint8, device=self.S.device)
+        # the fused bodies of a run as one persistent launch where the device holds every tile's
+        # workgroup at once (QSC_LOOP=0: the launch pairs); not with per-iteration NMSE tracking,
+        # which runs between the bodies
+        self.loop = (self.fuse and bool(loop) and not self.nmse_every
+                     and os.environ.get("QSC_LOOP", "1") != "0" and self.engine.scloop_supported())
 
     # one outer iteration = C grad-step + S grad-step
     def c_step(self):
@@ -258,6 +268,11 @@ class FreeSSolver:
         e.scpass(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s)
         self._track()  # (S_{i+1}, C_{i+1}): C is updated by the cfinish below
         e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)
+
+    def fused_loop(self, n):
+        """n fused bodies (fused_body x n) as one persistent launch: identical results."""
+        self.engine.scloop(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s,
+                           self.mC, self.vC, self.adam_c, self.lambda_c, n)
 
     def _track(self):
         if not self.nmse_every:
@@ -296,8 +311,16 @@ class FreeSSolver:
     def S_pixels(self):
         return self.obs.to_pixels(self.S, self.R).reshape(self.R, 1, self.obs.I, self.obs.J)
 
+    def check(self):
+        """Raise if a persistent-loop launch of this solver timed out at a grid barrier (its
+        workgroups were not all resident: the run's results are invalid, include/qsc.h)."""
+        if self.state().get("loop_fault"):
+            raise _lib.QscError("qsc_scloop: grid barrier timed out (workgroups not all "
+                                "resident); rerun with loop=False / QSC_LOOP=0")
+
     def history(self):
         self.engine.flush()  # settle the last S-pass (its history row)
+        self.check()
         st = self.state()
         n = min(int(st["iter"]), self.engine.hist_cap)
         h = self.engine.hist[: 4 * n].view(n, 4).double().cpu()
@@ -315,7 +338,8 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
           log_model=False, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2, max_iter=500,
           betas=(0.9, 0.999), eps=1e-8, project_c=True, generator=None, Z_init=None,
           restart=False, restart_samples=(200, 200), T_true=None, nmse_every=0,
-          use_graph=False, obs=None, tile=None, callback=None, loss="probit", fuse=True):
+          use_graph=False, obs=None, tile=None, callback=None, loss="probit", fuse=True,
+          loop=True):
     """Alternating S/C probit-MLE (qmc/qmc.ipynb :559-645).
 
     Args mirror the notebook globals: Y (K,1,I,J) bin indices, Wx (K,1,I,J) 0/1 mask,
@@ -349,7 +373,8 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
         # a callback still gets control every nmse_every iterations (or once at the end)
         sol = FreeSSolver(obs, S_init, C_init, lambda_c, lambda_s, lr_c, lr_s, betas, eps,
                           project_c, hist_cap=max_iter, fuse=fuse,
-                          T_true=T_true if nmse_every else None, nmse_every=nmse_every)
+                          T_true=T_true if nmse_every else None, nmse_every=nmse_every,
+                          loop=loop)
         done = 0
         chunk = nmse_every if (callback is not None and nmse_every) else max_iter
         while done < max_iter:
@@ -361,7 +386,8 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
         nmse = sol.nmse_history()
         costs_c, costs_s = sol.history()
         return SolveResult(S=sol.S_pixels(), C=sol.C.clone(), costs_c=costs_c, costs_s=costs_s,
-                           nmse=nmse, iters=max_iter, fused=sol.fuse)
+                           nmse=nmse, iters=max_iter, fused=sol.fuse,
+                           looped=sol.loop and max_iter >= 3)
     return _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c, lr_s,
                             max_iter, betas, eps, project_c, restart, restart_samples, T_true,
                             nmse_every, callback)

@@ -127,3 +127,33 @@ def test_integration_stub_error_path(libpath):
     ns = {"ctypes": ctypes, "_L": ctypes.CDLL(libpath)}
     exec(decl, ns)
     assert ns["_L"].qsc_error_string(_lib.QSC_EINVAL).decode() == "invalid argument"
+
+
+def _param_list(sig):
+    """The top-level parameter list of a demangled function signature."""
+    depth, end = 0, None
+    for i in range(len(sig) - 1, -1, -1):
+        c = sig[i]
+        if c == ")":
+            if depth == 0:
+                end = i
+            depth += 1
+        elif c == "(":
+            depth -= 1
+            if depth == 0:
+                return sig[i + 1:end]
+    return ""
+
+
+def test_kernels_take_no_reference_parameters(libpath):
+    """A __global__ function's reference parameter is passed as a host address that the device
+    then dereferences (a memory-access fault).  Every kernel of the library takes its structs by
+    value: scan the code object's kernel symbols (ours live in an anonymous namespace)."""
+    import re
+    data = open(libpath, "rb").read()
+    names = sorted(set(re.findall(rb"_ZN12_GLOBAL__N_1[0-9A-Za-z_]*_kernel[0-9A-Za-z_]*", data)))
+    assert len(names) > 20
+    out = subprocess.run(["c++filt"], input=b"\n".join(names), capture_output=True,
+                         check=True).stdout.decode().split("\n")
+    bad = [s for s in out if s and "&" in _param_list(s)]
+    assert not bad, bad[:3]

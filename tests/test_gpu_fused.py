@@ -495,3 +495,28 @@ def test_phase_split_fused_launch_is_bitexact():
     assert np.array_equal(a.S.cpu().numpy(), b.S.cpu().numpy())
     assert np.array_equal(a.C.cpu().numpy(), b.C.cpu().numpy())
     assert a.costs_c == b.costs_c and a.costs_s == b.costs_s
+
+
+@pytest.mark.parametrize("n", [2, 3, 11])
+def test_persistent_loop_is_bitexact(n):
+    """qsc_scloop (the fused bodies of a run as one persistent launch with grid barriers,
+    include/qsc.h) gives the launch pairs' S, C, moments, costs and state bit for bit, eager
+    and hipGraph, at the C3 shape class (1024-position tiles, 16-wave workgroups)."""
+    from quantized_spectrum_cartography_amd.obs import Observations
+    from quantized_spectrum_cartography_amd.qmc import FreeSSolver
+    d = _random_case(57, 8, 128, 128, 256)
+    o = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=8, tile=1024)
+    ref = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, loop=False)
+    assert ref.fuse and not ref.loop
+    ref.run(n)
+    for g in (False, True):
+        sol = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32)
+        assert sol.loop, "the persistent loop does not apply at this shape"
+        sol.run(n, use_graph=g)
+        for x, y in ((ref.S, sol.S), (ref.C, sol.C), (ref.mS, sol.mS), (ref.vS, sol.vS),
+                     (ref.mC, sol.mC), (ref.vC, sol.vC)):
+            assert torch.equal(x, y)
+        assert ref.history() == sol.history()
+        st = sol.state()
+        assert st["loop_fault"] == 0
+        assert {k: v for k, v in st.items()} == ref.state()
