@@ -215,7 +215,7 @@ class FreeSSolver:
 
     def __init__(self, obs, S_init, C_init, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
                  betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024, fuse=True,
-                 T_true=None, nmse_every=0, loop=True):
+                 T_true=None, nmse_every=0, loop=None):
         self.obs = obs
         R = S_init.shape[0]
         self.R = R
@@ -241,11 +241,14 @@ class FreeSSolver:
                                           dtype=torch.float64, device=self.S.device)
             self._nmse_ws = torch.empty(_lib.lib().qsc_reduce_workspace_bytes(0),
                                         dtype=torch.uint8, device=self.S.device)
-        # the fused bodies of a run as one persistent launch where the device holds every tile's
-        # workgroup at once (QSC_LOOP=0: the launch pairs); not with per-iteration NMSE tracking,
-        # which runs between the bodies
+        # the fused bodies of a run as one persistent launch (qsc_scloop) where the device holds
+        # every tile's workgroup at once; not with per-iteration NMSE tracking, which runs
+        # between the bodies.  loop=None: opt-in through QSC_LOOP=1 (off by default until the
+        # launch is validated on MI355X); loop=True/False forces it on/off
+        if loop is None:
+            loop = os.environ.get("QSC_LOOP", "0") == "1"
         self.loop = (self.fuse and bool(loop) and not self.nmse_every
-                     and os.environ.get("QSC_LOOP", "1") != "0" and self.engine.scloop_supported())
+                     and self.engine.scloop_supported())
 
     # one outer iteration = C grad-step + S grad-step
     def c_step(self):
@@ -339,7 +342,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
           betas=(0.9, 0.999), eps=1e-8, project_c=True, generator=None, Z_init=None,
           restart=False, restart_samples=(200, 200), T_true=None, nmse_every=0,
           use_graph=False, obs=None, tile=None, callback=None, loss="probit", fuse=True,
-          loop=True):
+          loop=None):
     """Alternating S/C probit-MLE (qmc/qmc.ipynb :559-645).
 
     Args mirror the notebook globals: Y (K,1,I,J) bin indices, Wx (K,1,I,J) 0/1 mask,

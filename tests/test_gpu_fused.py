@@ -502,6 +502,9 @@ def test_persistent_loop_is_bitexact(n):
     """qsc_scloop (the fused bodies of a run as one persistent launch with grid barriers,
     include/qsc.h) gives the launch pairs' S, C, moments, costs and state bit for bit, eager
     and hipGraph, at the C3 shape class (1024-position tiles, 16-wave workgroups)."""
+    import os
+    if os.environ.get("QSC_LOOP") != "1":
+        pytest.skip("persistent loop is opt-in (QSC_LOOP=1) until validated on MI355X")
     from quantized_spectrum_cartography_amd.obs import Observations
     from quantized_spectrum_cartography_amd.qmc import FreeSSolver
     d = _random_case(57, 8, 128, 128, 256)
@@ -510,7 +513,7 @@ def test_persistent_loop_is_bitexact(n):
     assert ref.fuse and not ref.loop
     ref.run(n)
     for g in (False, True):
-        sol = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32)
+        sol = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, loop=True)
         assert sol.loop, "the persistent loop does not apply at this shape"
         sol.run(n, use_graph=g)
         for x, y in ((ref.S, sol.S), (ref.C, sol.C), (ref.mS, sol.mS), (ref.vS, sol.vS),

@@ -17,7 +17,7 @@ def main():
     p = synthetic.onebit_problem(I, J, K, R, f=0.1, seed=5, keep_T=False)
     o = Observations(p["Y"], p["Wx"], p["b"], p["sigma"], R_hint=R)
     a = FreeSSolver(o, p["S0"], p["C0"], hist_cap=64, loop=False)
-    b = FreeSSolver(o, p["S0"], p["C0"], hist_cap=64)
+    b = FreeSSolver(o, p["S0"], p["C0"], hist_cap=64, loop=True)
     print("tiles", o.desc.ntiles, "loop applies", b.loop, flush=True)
     a.run(n)
     b.run(n)
