@@ -103,9 +103,10 @@ typedef struct qsc_state {
   float nll_c;      /* NLL of the last C-pass   (-sum Wx log P, qmc/qmc.ipynb :572) */
   float nll_s;      /* NLL of the last S-pass */
   float normsq_s_prev; /* ||S||^2 the last S-pass was evaluated with */
-  int32_t loop_fault;  /* sticky: 1 after a qsc_scloop launch whose grid barrier timed out
-                          (its workgroups were not all resident; results then invalid) */
-  float reserved[6];
+  int32_t fused_fault; /* sticky: 1 after a qsc_scpass_fin launch whose C-finish wait timed
+                          out (the launch's C update is then incomplete: results invalid) */
+  uint32_t fin_ticket; /* qsc_scpass_fin arrival counter (zeroed by qsc_state_init) */
+  float reserved[5];
 } qsc_state;
 
 /* Packed observation layout, produced by qsc_obs_layout (host struct).
@@ -353,24 +354,22 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
                        int32_t split_rows, const qsc_model* m, int32_t R, float* S,
                        const float* C, float* mS, float* vS, const qsc_adam* adam,
                        float lambda_s, qsc_state* st, void* ws, size_t ws_bytes, void* stream);
-/* Persistent fused loop: niter x (qsc_scpass, qsc_cfinish mode 1) in ONE launch -- the same
- * code, operands and summation order, so the same S, C, moments, state and history bit for bit
- * -- with a device-wide barrier after each half in place of the launch boundaries.  A solver
- * runs  cpass, cfinish, scloop(n-1), spass.  The workgroup of each pixel tile stays resident
- * for the whole launch, so it applies only where every tile's workgroup fits on the device at
- * once (qsc_scloop_supported: the fused launch at rank <= 8 with 16-wave workgroups and no more
- * tiles than compute units; qsc_scloop re-checks the occupancy and returns QSC_EINVAL rather
- * than launch otherwise).  A barrier wait that times out (the grid was not all resident after
- * all, e.g. another process holds CUs) sets st->loop_fault and the launch drains; the caller
- * must treat that run's results as invalid.  hist / hist_cap as qsc_cfinish. */
-QSC_API int qsc_scloop_supported(const qsc_obs_desc* d, int32_t R);
-QSC_API int qsc_scloop(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
-                       const int64_t* s_off, const void* c_entries, const int32_t* c_width,
-                       const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m, int32_t R,
-                       float* S, float* C, float* mS, float* vS, const qsc_adam* adam_s,
-                       float lambda_s, float* mC, float* vC, const qsc_adam* adam_c,
-                       float lambda_c, qsc_state* st, float* hist, int32_t hist_cap,
-                       int32_t niter, void* ws, size_t ws_bytes, void* stream);
+/* Fused S-step + next C-pass + that C-step's finish in ONE launch: qsc_scpass followed by
+ * qsc_cfinish(mode 1) -- the same code, operands and summation order, so the same S, C,
+ * moments, state and history bit for bit -- with the C-finish work items run by the last
+ * R*nks + 2 workgroups to finish their tiles (they wait for the rest; no co-residency needed).
+ * A solver then runs  cpass, cfinish, scpass_fin x (n-1), spass: one launch per iteration.
+ * Available when qsc_scpass_fin_supported(d, R): the fused launch at 16-wave workgroups with at
+ * least R*nks + 2 tiles.  st->fused_fault is set (sticky) if a wait timed out; the caller must
+ * then treat the run as invalid.  hist / hist_cap as qsc_cfinish. */
+QSC_API int qsc_scpass_fin_supported(const qsc_obs_desc* d, int32_t R);
+QSC_API int qsc_scpass_fin(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
+                           const int64_t* s_off, const void* c_entries, const int32_t* c_width,
+                           const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
+                           int32_t R, float* S, float* C, float* mS, float* vS,
+                           const qsc_adam* adam_s, float lambda_s, float* mC, float* vC,
+                           const qsc_adam* adam_c, float lambda_c, qsc_state* st, float* hist,
+                           int32_t hist_cap, void* ws, size_t ws_bytes, void* stream);
 /* reduce the C-pass slab (fixed order).  mode 0: write dC (NLL gradient only); mode 1: fused
  * C-step: dC + lambda_c*C/||C||, Adam on C, projection; mode 2 (IJ-slab sharding): as mode 0 and
  * dC[R*K] (dC holds R*K + 1 floats) receives this shard's ||S||^2 after the S-pass partials are

@@ -45,7 +45,7 @@ class QscObsDesc(ctypes.Structure):
                 ("rowfmt", ctypes.c_int32), ("reserved_", ctypes.c_int32)]
 
 
-# device-resident qsc_state: 4 int32 + 5 float + loop_fault int32 + 6 reserved float
+# device-resident qsc_state: 4 int32 + 5 float + fused_fault int32 + fin_ticket uint32 + 5 reserved
 STATE_BYTES = 64
 STATE_FIELDS = ("step_c", "step_s", "iter", "pending", "normsq_s", "normsq_c", "nll_c", "nll_s",
                 "normsq_s_prev")
@@ -200,7 +200,7 @@ def read_state(st):
     ints = raw[:16].view(torch.int32).tolist()
     flts = raw[16:36].view(torch.float32).tolist()
     out = dict(zip(STATE_FIELDS, ints + flts))
-    out["loop_fault"] = int(raw[36:40].view(torch.int32).item())
+    out["fused_fault"] = int(raw[36:40].view(torch.int32).item())
     return out
 
 

@@ -378,7 +378,15 @@ QSC_API int qsc_obs_layout(const uint8_t* codes, int32_t K, int32_t P, int32_t P
     return QSC_EINVAL;
   const int Pp = (int)round_up(P, PT);  // whole tiles; padding positions carry no entries
   const int ns = Pp / QSC_SLICE, nt = Pp / PT, nks = (int)ceil_div(K, 64);
-  if ((int64_t)nks * 64 * 2 * sizeof(int) > 128 * 1024) return QSC_EINVAL;  // LDS counts + order
+  // c_layout_kernel's LDS (counts + order, 2 ints per bin) against the device's own limit
+  int dev = 0, lds_max = 64 * 1024;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess &&
+        v > 0)
+      lds_max = v;
+  }
+  if ((int64_t)nks * 64 * 2 * sizeof(int) > lds_max) return QSC_EINVAL;
   const int wide = (K > 4096 || PT > 4096 || nbins > 15) ? 1 : 0;
   if (wide && ((int64_t)K >= (1 << 24) || (int64_t)PT >= (1 << 24))) return QSC_EINVAL;
   char* w = (char*)ws;

@@ -1430,61 +1430,8 @@ struct FusedBlock {
   s_ent, s_width, s_off, c_ent, c_width, c_off, c_kmap, nks, NP, PT, lk, E_, nbins, R, K, S, C, mS, \
       vS, ad, lambda_s, st, part_nll_s, part_nsq_s, slab, part_nll_c, cnsq, acache, c_split
 
-// the fused launch's operands as one struct (scloop_kernel reads them through the kernel
-// argument segment every iteration)
-template <typename E>
-struct ScfArgs {
-  const E* s_ent;
-  const int* s_width;
-  const int64_t* s_off;
-  const E* c_ent;
-  const int* c_width;
-  const int64_t* c_off;
-  const int* c_kmap;
-  int nks, NP, PT;
-  Lik lk;
-  Edges E_;
-  int nbins, R, K;
-  float* S;
-  const float* C;
-  float *mS, *vS;
-  qsc_adam ad;
-  float lambda_s;
-  qsc_state* st;
-  float *part_nll_s, *part_nsq_s, *slab, *part_nll_c, *cnsq;
-  AdamCache* acache;
-  const int* c_split;
-  // the C-finish half (scloop_kernel)
-  float *Cw, *mC, *vC;
-  qsc_adam adc;
-  float lambda_c;
-  float* hist;
-  int hist_cap;
-  AdamCache* acache_c;
-  int niter;
-  unsigned* bar;
-};
-// a by-value copy of a struct held in the kernel argument segment (scalar loads)
-template <typename T>
-__device__ __forceinline__ T ld_arg(const T __attribute__((address_space(4))) & x) {
-  static_assert(sizeof(T) % 4 == 0, "argument structs are whole dwords");
-  T out;
-  const uint32_t __attribute__((address_space(4)))* src =
-      (const uint32_t __attribute__((address_space(4)))*)&x;
-  uint32_t* dst = reinterpret_cast<uint32_t*>(&out);
-#pragma unroll
-  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = src[i];
-  return out;
-}
-#define QSC_SCF_ARGS_OF(a)                                                                     \
-  a.s_ent, a.s_width, a.s_off, a.c_ent, a.c_width, a.c_off, a.c_kmap, a.nks, a.NP, a.PT,        \
-      ld_arg<Lik>(a.lk), *(const Edges*)(&a.E_), a.nbins, a.R, a.K, a.S, a.C, a.mS, a.vS,       \
-      ld_arg<qsc_adam>(a.ad), a.lambda_s, a.st, a.part_nll_s, a.part_nsq_s, a.slab,              \
-      a.part_nll_c, a.cnsq, a.acache, a.c_split
-
-// One pixel tile t of nt of the fused launch (scfused_kernel: t = the workgroup; scloop_kernel:
-// the same tile every iteration; C is read-only within a call -- the loop kernel's C-finish
-// writes it between calls, behind grid barriers).
+// One pixel tile t of nt of the fused launch (scfused_kernel, scfin_kernel: t = the workgroup).
+// C is read-only here; scfin_kernel's C-finish writes it after every tile has finished.
 template <int RP, typename E, int KIND, bool LOG>
 __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const int nt) {
   using V4 = typename Ent<E>::V4;
@@ -1933,8 +1880,8 @@ __device__ void settle_s(qsc_state* __restrict__ st, const float* __restrict__ p
       npart_c, part_nll_s, part_nsq_s, nslices, hist, hist_cap, acache
 constexpr int kFWaves = kFBlock / 64;
 
-// C-finish work item vb of R*nks + 2 (cfinish_kernel: vb = the workgroup; scloop_kernel: the
-// workgroups' share of them after a grid barrier), with its LDS scratch passed in
+// C-finish work item vb of R*nks + 2 (cfinish_kernel: vb = the workgroup; scfin_kernel: one
+// item per late-arriving workgroup), with its LDS scratch passed in
 __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scalars& sc,
                                            float (*sh3)[kFWaves], QSC_CF_PARAMS) {
   constexpr int NW = kFWaves;
@@ -2077,85 +2024,64 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(QSC_CF_PARAMS) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Persistent fused loop: n outer iterations of (scpass, cfinish) in one launch
+// Fused launch with the C-finish at its tail (qsc_scpass_fin)
 // ---------------------------------------------------------------------------------------
-// The workgroup of tile t keeps that tile for every iteration: S-step i + C-pass i+1 of the
-// tile (scfused_tile), grid barrier, its share of the C-finish work items (cfinish_vb), grid
-// barrier.  Same code, same operands, same order as the launch pair, so the results are those
-// of (qsc_scpass, qsc_cfinish) x n bit for bit; what goes is the pair's launch ramps and the
-// C-finish's own dispatch.  qsc_scloop launches it only when every workgroup is resident at
-// once (one per CU at C3), which the barriers need.
-//
-// Grid barrier: every thread makes its writes visible device-wide (agent-scope fence), the
-// workgroup meets, one thread adds its arrival to the launch's counter (device-scope atomic)
-// and polls it (acquire loads) until `target`; the workgroup then meets again behind an
-// agent-scope fence.  A wait longer than kLoopSpin polls (a grid that is not all resident)
-// raises the sticky loop_fault word of the state and every workgroup leaves the launch at its
-// next barrier, so the grid always drains; the host reports the fault (read_state).
-constexpr unsigned kLoopSpin = 1u << 20;
-
-__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, int* fault, int* okl) {
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int ok = 1;
-    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned polls = 0;
-    while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (__hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-        ok = 0;
-        break;
-      }
-      if (++polls > kLoopSpin) {
-        __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    *okl = ok;
-  }
-  __syncthreads();
-  const bool ok = *okl != 0;
-  __threadfence();
-  return ok;
-}
+// scfused_tile, then each workgroup takes an arrival ticket (device-scope atomic on the state's
+// fin_ticket word, after its writes are made visible device-wide); the LAST R*nks + 2 arrivals
+// wait until every tile has arrived and then run the C-finish work items (cfinish_vb), the
+// earlier ones leave.  The C-step finish that was a launch of its own rides on the tail of the
+// fused launch: same code, operands and order as (qsc_scpass, qsc_cfinish mode 1), so the same
+// results bit for bit, one launch per iteration instead of two.  No co-residency is needed:
+// a waiting workgroup is one of the last R*nks + 2 to arrive, so at most R*nks + 1 others are
+// still to come, and the workgroups that already left free their CUs for them.  Tickets count
+// up for the life of the state (it is zeroed with it); launch j's arrivals hold tickets
+// [j*nt, (j+1)*nt).  A wait past kFinSpin polls (cannot happen unless the device is shared
+// with other work that holds every CU) sets the state's sticky fault word and skips the item.
+constexpr unsigned kFinSpin = 1u << 20;
 
 template <int RP, typename E, int KIND, bool LOG>
-__global__ void __launch_bounds__(FusedBlock<RP>::v) scloop_kernel(const ScfArgs<E> args) {
+__global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
+    QSC_SCF_KPARAMS, float* Cw, float* __restrict__ mC, float* __restrict__ vC, qsc_adam adc,
+    float lambda_c, float* __restrict__ hist, int hist_cap, AdamCache* __restrict__ acache_c) {
+  scfused_tile<RP, E, KIND, LOG>(QSC_SCF_ARGS, (int)blockIdx.x, (int)gridDim.x);
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  using KArgs = const ScfArgs<E> __attribute__((address_space(4)));
-  const int t = blockIdx.x, nt = gridDim.x;
-  // C-finish scratch and the barrier's broadcast word, over the (then idle) tile LDS
+  const int nt = gridDim.x, nvb = R * nks + 2;
+  // C-finish scratch and the arrival broadcast word, over the (now idle) tile LDS
   float(*red)[64] = reinterpret_cast<float(*)[64]>(smem);
   float(*sh3)[kFWaves] = reinterpret_cast<float(*)[kFWaves]>(smem + kFWaves * 64);
   Scalars& sc = *reinterpret_cast<Scalars*>(smem + kFWaves * 64 + 3 * kFWaves);
-  int* okl = reinterpret_cast<int*>(smem + kFWaves * 64 + 3 * kFWaves + 16);
-  unsigned target = 0;
-  for (int it = 0; it < args.niter; ++it) {
-    // the operands are re-read from the argument segment each iteration (an opaque pointer to
-    // it): held across iterations they would need more scalar registers than there are
-    KArgs* ap = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
-    asm volatile("" : "+s"(ap));
-    scfused_tile<RP, E, KIND, LOG>(QSC_SCF_ARGS_OF((*ap)), t, nt);
-    // (a second opaque pointer: the C-finish half re-reads what it needs instead of keeping
-    // the tile half's operands live through the whole tile)
-    KArgs* bp = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
-    asm volatile("" : "+s"(bp));
-    KArgs& a = *bp;
-    int* fault = reinterpret_cast<int*>(a.st) + 9;  // qsc_state.loop_fault
-    target += (unsigned)nt;
-    if (!grid_sync(a.bar, target, fault, okl)) return;
-    for (int vb = t; vb < a.R * a.nks + 2; vb += nt) {
-      cfinish_vb(vb, red, sc, sh3, a.slab, nt, a.nks, a.R, a.K, a.Cw, 1, nullptr, a.mC, a.vC,
-                 ld_arg<qsc_adam>(a.adc), a.lambda_c, nullptr, a.cnsq, a.st, a.part_nll_c, nt * a.nks,
-                 a.part_nll_s, a.part_nsq_s, nt * a.PT / QSC_SLICE, a.hist, a.hist_cap,
-                 a.acache_c);
-      __syncthreads();
+  int* vbl = reinterpret_cast<int*>(smem + kFWaves * 64 + 3 * kFWaves + 16);
+  unsigned* ticket = reinterpret_cast<unsigned*>(st) + 10;  // qsc_state.fin_ticket
+  int* fault = reinterpret_cast<int*>(st) + 9;              // qsc_state.fused_fault
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned tk =
+        __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned a = tk % (unsigned)nt;
+    int vb = (int)a - (nt - nvb);
+    if (vb >= 0) {
+      const unsigned target = tk - a + (unsigned)nt;
+      unsigned polls = 0;
+      while ((int)(__hip_atomic_load(ticket, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) -
+                   target) < 0) {
+        if (++polls > kFinSpin) {
+          __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          vb = -1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
     }
-    target += (unsigned)nt;
-    if (!grid_sync(a.bar, target, fault, okl)) return;
+    *vbl = vb;
   }
+  __syncthreads();
+  const int vb = *vbl;
+  if (vb < 0) return;
+  __threadfence();
+  cfinish_vb(vb, red, sc, sh3, slab, nt, nks, R, K, Cw, 1, nullptr, mC, vC, adc, lambda_c,
+             nullptr, cnsq, st, part_nll_c, nt * nks, part_nll_s, part_nsq_s,
+             nt * PT / QSC_SLICE, hist, hist_cap, acache_c);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2346,7 +2272,6 @@ struct PassWs {
   int* sched;       // S-pass queue counters [kSchedQ] + finished-wave counter (zero between launches)
   float* cnsq;      // ||C||^2 of the C the last C-pass read (written by the C-pass)
   AdamCache* acache;  // [0..1] S-side, [2..3] C-side step scalars (adam_scalars_cached)
-  unsigned* bar;      // scloop_kernel's grid-barrier arrivals (zeroed before each launch)
 };
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -2370,8 +2295,6 @@ PassWs carve(const qsc_obs_desc* d, int R, void* ws) {
   p.cnsq = (float*)w;
   w += al(4);
   p.acache = (AdamCache*)w;
-  w += al(4 * sizeof(AdamCache));
-  p.bar = (unsigned*)w;
   return p;
 }
 
@@ -2379,7 +2302,7 @@ size_t ws_bytes_for(const qsc_obs_desc* d, int R) {
   const int64_t Kp = (int64_t)d->nks * 64;
   return al((size_t)d->ntiles * R * Kp * 4) + al((size_t)d->ntiles * d->nks * 4) +
          2 * al((size_t)(d->Pp / QSC_SLICE) * 4) + al(256 * 8) + al((kSchedQ + 1) * 4) + al(4) +
-         al(4 * sizeof(AdamCache)) + al(4);
+         al(4 * sizeof(AdamCache));
 }
 
 bool desc_ok(const qsc_obs_desc* d) {
@@ -2455,6 +2378,13 @@ int spass_bpc(int RP) { return RP > 8 ? 2 : RP == 8 ? QSC_SPASS_BPC8 : QSC_SPASS
     else if (RP == 8) LAUNCH(8, uint16_t, KD, LG);                                       \
     else LAUNCH(16, uint16_t, KD, LG);                                                   \
   } while (0)
+#ifdef QSC_DEV_ONE_VARIANT  // (ISA work: only the C3 signed-row rank-8 instantiation)
+#define QSC_DISPATCH_PASS(LAUNCH)                   \
+  do {                                              \
+    (void)kind;                                     \
+    if (sr && RP == 8) LAUNCH(8, uint16_t, LIK_ONEBIT_SR, false); \
+  } while (0)
+#else
 #define QSC_DISPATCH_PASS(LAUNCH)                                                        \
   do {                                                                                   \
     if (sr) QSC_DISPATCH_RP_NARROW(LAUNCH, LIK_ONEBIT_SR, false);                        \
@@ -2464,42 +2394,9 @@ int spass_bpc(int RP) { return RP > 8 ? 2 : RP == 8 ? QSC_SPASS_BPC8 : QSC_SPASS
     else if (m->log_model) QSC_DISPATCH_RP(LAUNCH, LIK_GENERAL, true);                   \
     else QSC_DISPATCH_RP(LAUNCH, LIK_GENERAL, false);                                    \
   } while (0)
+#endif
 
 static bool rowfmt_ok(const qsc_obs_desc* d, int R, int kind);
-static unsigned scpass_threads(const qsc_obs_desc* d, int R);
-static int cpass_parts(const qsc_obs_desc* d, int R, bool sr);
-
-// one scloop_kernel launch (rank <= 8: 16-wave workgroups, the C-finish's width), after
-// checking that the whole grid is resident at once
-template <int RPV, typename ET, int KD, bool LG>
-static int scloop_launch(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
-                         const int64_t* s_off, const void* c_entries, const int32_t* c_width,
-                         const int64_t* c_off, const int32_t* c_kmap, int NP, const Lik& lk,
-                         const Edges& E, int R, float* S, float* C, float* mS, float* vS,
-                         const qsc_adam& ad, float lambda_s, float* mC, float* vC,
-                         const qsc_adam& adc, float lambda_c, qsc_state* st, float* hist,
-                         int hist_cap, int niter, const PassWs& w, unsigned threads, size_t shm,
-                         hipStream_t s) {
-  if constexpr (RPV > 8) {
-    return QSC_EINVAL;
-  } else {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &nb, reinterpret_cast<const void*>(&scloop_kernel<RPV, ET, KD, LG>), (int)threads,
-            shm) != hipSuccess ||
-        (int64_t)nb * cu_count() < d->ntiles)
-      return QSC_EINVAL;
-    QSC_TRY(hipMemsetAsync(w.bar, 0, sizeof(unsigned), s));
-    ScfArgs<ET> a{(const ET*)s_entries, s_width, s_off, (const ET*)c_entries, c_width, c_off,
-                  c_kmap, d->nks, NP, d->PT, lk, E, d->nbins, R, d->K, S, C, mS, vS, ad,
-                  lambda_s, st, w.snll, w.snsq, w.slab, w.cnll, w.cnsq, w.acache, nullptr, C,
-                  mC, vC, adc, lambda_c, hist, hist_cap, w.acache + 2, niter, w.bar};
-    hipLaunchKernelGGL((scloop_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles), dim3(threads),
-                       shm, s, a);
-    QSC_CHECK_LAUNCH();
-    return QSC_OK;
-  }
-}
 
 extern "C" {
 
@@ -2764,25 +2661,25 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
   return QSC_OK;
 }
 
-QSC_API int qsc_scloop_supported(const qsc_obs_desc* d, int32_t R) {
-  if (!qsc_scpass_supported(d, R) || rp_of(R) > 8) return 0;
-  return (scpass_threads(d, R) == (unsigned)kFBlock && d->ntiles <= cu_count()) ? 1 : 0;
+QSC_API int qsc_scpass_fin_supported(const qsc_obs_desc* d, int32_t R) {
+  if (!qsc_scpass_supported(d, R)) return 0;
+  // the C-finish work items run on 16-wave workgroups, one item per late arrival
+  return (scpass_threads(d, R) == (unsigned)kFBlock && d->ntiles >= R * d->nks + 2) ? 1 : 0;
 }
 
-QSC_API int qsc_scloop(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
-                       const int64_t* s_off, const void* c_entries, const int32_t* c_width,
-                       const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m, int32_t R,
-                       float* S, float* C, float* mS, float* vS, const qsc_adam* adam_s,
-                       float lambda_s, float* mC, float* vC, const qsc_adam* adam_c,
-                       float lambda_c, qsc_state* st, float* hist, int32_t hist_cap,
-                       int32_t niter, void* ws, size_t ws_bytes, void* stream) {
-  if (!qsc_scloop_supported(d, R) || !m || m->nbounds - 1 != d->nbins || !S || !C || !mS ||
+QSC_API int qsc_scpass_fin(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
+                           const int64_t* s_off, const void* c_entries, const int32_t* c_width,
+                           const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
+                           int32_t R, float* S, float* C, float* mS, float* vS,
+                           const qsc_adam* adam_s, float lambda_s, float* mC, float* vC,
+                           const qsc_adam* adam_c, float lambda_c, qsc_state* st, float* hist,
+                           int32_t hist_cap, void* ws, size_t ws_bytes, void* stream) {
+  if (!qsc_scpass_fin_supported(d, R) || !m || m->nbounds - 1 != d->nbins || !S || !C || !mS ||
       !vS || !adam_s || !mC || !vC || !adam_c || !st || !s_width || !s_off || !c_width ||
       !c_off || !c_kmap || (d->s_entries > 0 && !s_entries) ||
-      (d->c_entries > 0 && !c_entries) || !ws || ws_bytes < ws_bytes_for(d, R) || niter < 0 ||
+      (d->c_entries > 0 && !c_entries) || !ws || ws_bytes < ws_bytes_for(d, R) ||
       (hist_cap > 0 && !hist))
     return QSC_EINVAL;
-  if (niter == 0) return QSC_OK;
   const int RP = rp_of(R);
   const int kind = lik_kind(m);
   const bool sr = d->rowfmt == 1;
@@ -2798,17 +2695,24 @@ QSC_API int qsc_scloop(const qsc_obs_desc* d, const void* s_entries, const int32
     make_sq_targets(m, &E);
   else if (!m->log_model)
     scale_edges(&E, m->nbounds - 1, lk.a);
+  const qsc_adam ad = *adam_s, adc = *adam_c;
   const unsigned threads = scpass_threads(d, R);
+  (void)RP;
   hipStream_t s = STREAM(stream);
-  int rc = QSC_EINVAL;
-#define SCLOOP_LAUNCH(RPV, ET, KD, LG)                                                         \
-  rc = scloop_launch<RPV, ET, KD, LG>(d, s_entries, s_width, s_off, c_entries, c_width, c_off,  \
-                                      c_kmap, NP, lk, E, R, S, C, mS, vS, *adam_s, lambda_s,   \
-                                      mC, vC, *adam_c, lambda_c, st, hist, hist_cap, niter, w,  \
-                                      threads, shm, s)
-  QSC_DISPATCH_PASS(SCLOOP_LAUNCH);
-#undef SCLOOP_LAUNCH
-  return rc;
+#define SCFIN_LAUNCH(RPV, ET, KD, LG)                                                          \
+  do {                                                                                         \
+    if constexpr (RPV <= 8)                                                                    \
+      hipLaunchKernelGGL((scfin_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles),           \
+                         dim3(threads), shm, s, (const ET*)s_entries, s_width, s_off,          \
+                         (const ET*)c_entries, c_width, c_off, c_kmap, d->nks, NP, d->PT, lk,  \
+                         E, d->nbins, R, d->K, S, C, mS, vS, ad, lambda_s, st, w.snll, w.snsq, \
+                         w.slab, w.cnll, w.cnsq, w.acache, (const int*)nullptr, C, mC, vC,     \
+                         adc, lambda_c, hist, hist_cap, w.acache + 2);                         \
+  } while (0)
+  QSC_DISPATCH_PASS(SCFIN_LAUNCH);
+#undef SCFIN_LAUNCH
+  QSC_CHECK_LAUNCH();
+  return QSC_OK;
 }
 
 QSC_API int qsc_cfinish(const qsc_obs_desc* d, int32_t R, float* C, int32_t mode, float* dC,

@@ -89,21 +89,21 @@ class PassEngine:
                   _lib.ptr(vS), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),
                   self.ws.numel(), _lib.stream())
 
-    def scloop_supported(self):
-        return bool(_lib.lib().qsc_scloop_supported(self.desc, self.R))
+    def scpass_fin_supported(self):
+        return bool(_lib.lib().qsc_scpass_fin_supported(self.desc, self.R))
 
-    def scloop(self, S_pos, C, mS, vS, adam_s, lambda_s, mC, vC, adam_c, lambda_c, n,
-               record=True):
-        """n x (scpass, cfinish mode 1) in one persistent launch (qsc_scloop): the same results
-        bit for bit, without the launch pair's ramps."""
+    def scpass_fin(self, S_pos, C, mS, vS, adam_s, lambda_s, mC, vC, adam_c, lambda_c,
+                   record=True):
+        """scpass followed by cfinish (mode 1) in ONE launch (qsc_scpass_fin): the C-step finish
+        runs on the last workgroups to finish their tiles; the same results bit for bit."""
         o = self.obs
         hist, cap = (self.hist, self.hist_cap) if (record and self.hist_cap) else (None, 0)
-        _lib.call("qsc_scloop", self.desc, _lib.ptr(self.s_entries), _lib.ptr(o.s_width),
+        _lib.call("qsc_scpass_fin", self.desc, _lib.ptr(self.s_entries), _lib.ptr(o.s_width),
                   _lib.ptr(o.s_off), _lib.ptr(self.c_entries), _lib.ptr(o.c_width),
                   _lib.ptr(o.c_off), _lib.ptr(o.c_kmap), o.model, self.R, _lib.ptr(S_pos),
                   _lib.ptr(C), _lib.ptr(mS), _lib.ptr(vS), adam_s, float(lambda_s), _lib.ptr(mC),
                   _lib.ptr(vC), adam_c, float(lambda_c), _lib.ptr(self.state), _lib.ptr(hist),
-                  cap, int(n), _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
+                  cap, _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
 
     def supdate(self, S_pos, mS, vS, g, adam, lambda_s):
         _lib.call("qsc_supdate", self.desc, self.R, _lib.ptr(S_pos), _lib.ptr(mS), _lib.ptr(vS),

@@ -38,7 +38,7 @@ class SolveResult:
     Z: Optional[torch.Tensor] = None
     iters: int = 0
     fused: bool = False                 # S-step + next C-pass ran as one launch (qsc_scpass)
-    looped: bool = False                # the fused bodies ran as one persistent launch (qsc_scloop)
+    fin: bool = False                   # ... with the C-step finish in the same launch
 
 
 # Longest run captured as one hipGraph; longer runs replay several (results are identical:
@@ -52,11 +52,8 @@ def issue_iterations(solver, n):
     finish): c_step, fused_body x (n-1), s_step -- two launches per iteration."""
     if getattr(solver, "fuse", False) and n >= 2:
         solver.c_step()
-        if getattr(solver, "loop", False):
-            solver.fused_loop(n - 1)  # the n-1 bodies as one persistent launch (qsc_scloop)
-        else:
-            for _ in range(n - 1):
-                solver.fused_body()
+        for _ in range(n - 1):
+            solver.fused_body()
         solver.s_step()
     else:
         for _ in range(n):
@@ -215,7 +212,7 @@ class FreeSSolver:
 
     def __init__(self, obs, S_init, C_init, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
                  betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024, fuse=True,
-                 T_true=None, nmse_every=0, loop=None):
+                 T_true=None, nmse_every=0, fin=None):
         self.obs = obs
         R = S_init.shape[0]
         self.R = R
@@ -241,14 +238,14 @@ class FreeSSolver:
                                           dtype=torch.float64, device=self.S.device)
             self._nmse_ws = torch.empty(_lib.lib().qsc_reduce_workspace_bytes(0),
                                         dtype=torch.uint8, device=self.S.device)
-        # the fused bodies of a run as one persistent launch (qsc_scloop) where the device holds
-        # every tile's workgroup at once; not with per-iteration NMSE tracking, which runs
-        # between the bodies.  loop=None: opt-in through QSC_LOOP=1 (off by default until the
-        # launch is validated on MI355X); loop=True/False forces it on/off
-        if loop is None:
-            loop = os.environ.get("QSC_LOOP", "0") == "1"
-        self.loop = (self.fuse and bool(loop) and not self.nmse_every
-                     and self.engine.scloop_supported())
+        # the fused body's C-step finish on the tail of its own launch (qsc_scpass_fin: one
+        # launch per iteration); not with per-iteration NMSE tracking, which runs between the
+        # S-step and that finish.  fin=None: opt-in through QSC_FIN=1 (off by default until the
+        # launch is validated on MI355X); fin=True/False forces it on/off
+        if fin is None:
+            fin = os.environ.get("QSC_FIN", "0") == "1"
+        self.fin = (self.fuse and bool(fin) and not self.nmse_every
+                    and self.engine.scpass_fin_supported())
 
     # one outer iteration = C grad-step + S grad-step
     def c_step(self):
@@ -266,16 +263,16 @@ class FreeSSolver:
         self.s_step()
 
     def fused_body(self):
-        """S-step i fused with C-pass i+1, then C-step i+1's finish (needs a C-step before)."""
+        """S-step i fused with C-pass i+1, then C-step i+1's finish (needs a C-step before);
+        with `fin` all three in one launch."""
         e = self.engine
+        if self.fin:
+            e.scpass_fin(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s, self.mC,
+                         self.vC, self.adam_c, self.lambda_c)
+            return
         e.scpass(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s)
         self._track()  # (S_{i+1}, C_{i+1}): C is updated by the cfinish below
         e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)
-
-    def fused_loop(self, n):
-        """n fused bodies (fused_body x n) as one persistent launch: identical results."""
-        self.engine.scloop(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s,
-                           self.mC, self.vC, self.adam_c, self.lambda_c, n)
 
     def _track(self):
         if not self.nmse_every:
@@ -315,11 +312,11 @@ class FreeSSolver:
         return self.obs.to_pixels(self.S, self.R).reshape(self.R, 1, self.obs.I, self.obs.J)
 
     def check(self):
-        """Raise if a persistent-loop launch of this solver timed out at a grid barrier (its
-        workgroups were not all resident: the run's results are invalid, include/qsc.h)."""
-        if self.state().get("loop_fault"):
-            raise _lib.QscError("qsc_scloop: grid barrier timed out (workgroups not all "
-                                "resident); rerun with loop=False / QSC_LOOP=0")
+        """Raise if a fused-finish launch of this solver timed out waiting for the other tiles
+        (the run's C updates are then incomplete, include/qsc.h qsc_scpass_fin)."""
+        if self.state().get("fused_fault"):
+            raise _lib.QscError("qsc_scpass_fin: the C-finish wait timed out; rerun with "
+                                "fin=False / QSC_FIN=0")
 
     def history(self):
         self.engine.flush()  # settle the last S-pass (its history row)
@@ -342,7 +339,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
           betas=(0.9, 0.999), eps=1e-8, project_c=True, generator=None, Z_init=None,
           restart=False, restart_samples=(200, 200), T_true=None, nmse_every=0,
           use_graph=False, obs=None, tile=None, callback=None, loss="probit", fuse=True,
-          loop=None):
+          fin=None):
     """Alternating S/C probit-MLE (qmc/qmc.ipynb :559-645).
 
     Args mirror the notebook globals: Y (K,1,I,J) bin indices, Wx (K,1,I,J) 0/1 mask,
@@ -377,7 +374,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
         sol = FreeSSolver(obs, S_init, C_init, lambda_c, lambda_s, lr_c, lr_s, betas, eps,
                           project_c, hist_cap=max_iter, fuse=fuse,
                           T_true=T_true if nmse_every else None, nmse_every=nmse_every,
-                          loop=loop)
+                          fin=fin)
         done = 0
         chunk = nmse_every if (callback is not None and nmse_every) else max_iter
         while done < max_iter:
@@ -390,7 +387,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
         costs_c, costs_s = sol.history()
         return SolveResult(S=sol.S_pixels(), C=sol.C.clone(), costs_c=costs_c, costs_s=costs_s,
                            nmse=nmse, iters=max_iter, fused=sol.fuse,
-                           looped=sol.loop and max_iter >= 3)
+                           fin=sol.fin and max_iter >= 2)
     return _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c, lr_s,
                             max_iter, betas, eps, project_c, restart, restart_samples, T_true,
                             nmse_every, callback)

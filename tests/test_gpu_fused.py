@@ -498,28 +498,30 @@ def test_phase_split_fused_launch_is_bitexact():
 
 
 @pytest.mark.parametrize("n", [2, 3, 11])
-def test_persistent_loop_is_bitexact(n):
-    """qsc_scloop (the fused bodies of a run as one persistent launch with grid barriers,
-    include/qsc.h) gives the launch pairs' S, C, moments, costs and state bit for bit, eager
-    and hipGraph, at the C3 shape class (1024-position tiles, 16-wave workgroups)."""
+@pytest.mark.parametrize("shape", [(8, 192, 192, 256), (4, 128, 128, 64)])
+def test_fused_finish_is_bitexact(n, shape):
+    """qsc_scpass_fin (S-step + next C-pass + that C-step's finish in one launch, the finish on
+    the last workgroups to arrive, include/qsc.h) gives the launch pairs' S, C, moments, costs
+    and state bit for bit, eager and hipGraph."""
     import os
-    if os.environ.get("QSC_LOOP") != "1":
-        pytest.skip("persistent loop is opt-in (QSC_LOOP=1) until validated on MI355X")
+    if os.environ.get("QSC_FIN") != "1":
+        pytest.skip("the fused-finish launch is opt-in (QSC_FIN=1) until validated on MI355X")
     from quantized_spectrum_cartography_amd.obs import Observations
     from quantized_spectrum_cartography_amd.qmc import FreeSSolver
-    d = _random_case(57, 8, 128, 128, 256)
-    o = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=8, tile=1024)
-    ref = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, loop=False)
-    assert ref.fuse and not ref.loop
+    R, I, J, K = shape
+    d = _random_case(57, R, I, J, K)
+    o = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=R, tile=1024)
+    ref = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, fin=False)
+    assert ref.fuse and not ref.fin
     ref.run(n)
     for g in (False, True):
-        sol = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, loop=True)
-        assert sol.loop, "the persistent loop does not apply at this shape"
+        sol = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, fin=True)
+        assert sol.fin, "the fused-finish launch does not apply at this shape"
         sol.run(n, use_graph=g)
         for x, y in ((ref.S, sol.S), (ref.C, sol.C), (ref.mS, sol.mS), (ref.vS, sol.vS),
                      (ref.mC, sol.mC), (ref.vC, sol.vC)):
             assert torch.equal(x, y)
         assert ref.history() == sol.history()
-        st = sol.state()
-        assert st["loop_fault"] == 0
-        assert {k: v for k, v in st.items()} == ref.state()
+        st, rs = sol.state(), ref.state()
+        assert st["fused_fault"] == 0
+        assert st == rs
