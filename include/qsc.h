@@ -105,8 +105,8 @@ typedef struct qsc_state {
   float normsq_s_prev; /* ||S||^2 the last S-pass was evaluated with */
   int32_t fused_fault; /* sticky: 1 after a qsc_scpass_fin launch whose C-finish wait timed
                           out (the launch's C update is then incomplete: results invalid) */
-  uint32_t fin_ticket; /* qsc_scpass_fin arrival counter (zeroed by qsc_state_init) */
-  float reserved[5];
+  uint64_t fin_ticket; /* qsc_scpass_fin arrival counter, never wraps (zeroed by qsc_state_init) */
+  float reserved[4];
 } qsc_state;
 
 /* Packed observation layout, produced by qsc_obs_layout (host struct).

@@ -45,7 +45,7 @@ class QscObsDesc(ctypes.Structure):
                 ("rowfmt", ctypes.c_int32), ("reserved_", ctypes.c_int32)]
 
 
-# device-resident qsc_state: 4 int32 + 5 float + fused_fault int32 + fin_ticket uint32 + 5 reserved
+# device-resident qsc_state: 4 int32 + 5 float + fused_fault int32 + fin_ticket uint64 + 4 reserved
 STATE_BYTES = 64
 STATE_FIELDS = ("step_c", "step_s", "iter", "pending", "normsq_s", "normsq_c", "nll_c", "nll_s",
                 "normsq_s_prev")

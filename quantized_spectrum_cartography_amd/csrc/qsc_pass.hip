@@ -2051,20 +2051,21 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
   float(*sh3)[kFWaves] = reinterpret_cast<float(*)[kFWaves]>(smem + kFWaves * 64);
   Scalars& sc = *reinterpret_cast<Scalars*>(smem + kFWaves * 64 + 3 * kFWaves);
   int* vbl = reinterpret_cast<int*>(smem + kFWaves * 64 + 3 * kFWaves + 16);
-  unsigned* ticket = reinterpret_cast<unsigned*>(st) + 10;  // qsc_state.fin_ticket
+  // qsc_state.fin_ticket (64-bit: it counts every workgroup of every launch for the life of
+  // the state, and must stay aligned to launches, so it may never wrap)
+  unsigned long long* ticket = reinterpret_cast<unsigned long long*>(st) + 5;
   int* fault = reinterpret_cast<int*>(st) + 9;              // qsc_state.fused_fault
   __threadfence();
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned tk =
-        __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned a = tk % (unsigned)nt;
+    const unsigned long long tk =
+        __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long a = tk % (unsigned long long)nt;
     int vb = (int)a - (nt - nvb);
     if (vb >= 0) {
-      const unsigned target = tk - a + (unsigned)nt;
+      const unsigned long long target = tk - a + (unsigned long long)nt;
       unsigned polls = 0;
-      while ((int)(__hip_atomic_load(ticket, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) -
-                   target) < 0) {
+      while (__hip_atomic_load(ticket, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
         if (++polls > kFinSpin) {
           __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           vb = -1;

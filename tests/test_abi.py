@@ -52,8 +52,10 @@ def test_struct_layouts_match_c():
 #include <stddef.h>
 #include "qsc.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(qsc_model), sizeof(qsc_adam), sizeof(qsc_obs_desc),
-         sizeof(qsc_state), offsetof(qsc_model, bounds), offsetof(qsc_obs_desc, nnz));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(qsc_model), sizeof(qsc_adam),
+         sizeof(qsc_obs_desc), sizeof(qsc_state), offsetof(qsc_model, bounds),
+         offsetof(qsc_obs_desc, nnz), offsetof(qsc_state, fused_fault),
+         offsetof(qsc_state, fin_ticket));
   return 0;
 }
 '''
@@ -69,6 +71,9 @@ int main(void) {
     assert vals[3] == _lib.STATE_BYTES
     assert vals[4] == _lib.QscModel.bounds.offset
     assert vals[5] == _lib.QscObsDesc.nnz.offset
+    # the words the fused-finish launch addresses by index (csrc/qsc_pass.hip scfin_kernel:
+    # int word 9, 64-bit word 5) and _lib.read_state decodes
+    assert vals[6] == 36 and vals[7] == 40
 
 
 def test_product_fails_loudly_without_gpu():

@@ -58,3 +58,27 @@ def test_every_package_module_imports():
         if m.name.startswith("libqsc"):  # (the HIP libraries, loaded through ctypes)
             continue
         importlib.import_module("%s.%s" % (pkg.__name__, m.name))
+
+
+def _fin_roles(tickets, nt, nvb):
+    """The fused-finish arrival protocol of scfin_kernel (csrc/qsc_pass.hip), restated: a
+    workgroup holding ticket tk (64-bit, never wraps) is arrival a = tk mod nt of its launch; the
+    last nvb arrivals run C-finish item a - (nt - nvb) once the counter reaches tk - a + nt."""
+    return [(tk % nt - (nt - nvb), tk - tk % nt + nt) for tk in tickets]
+
+
+def test_fused_finish_ticket_protocol():
+    """Every launch's last R*nks + 2 arrivals take each C-finish item exactly once, all of them
+    wait for the same count -- the launch's last ticket + 1 -- and the earlier arrivals leave;
+    over consecutive launches of any tile count (tickets count up for the life of the state)."""
+    for nt, nvb in ((256, 34), (64, 6), (34, 34), (36, 34), (1000, 130)):
+        for start_launch in (0, 7, 10 ** 12):
+            for launch in range(3):
+                first = (start_launch + launch) * nt
+                tickets = [first + i for i in range(nt)]  # in arrival order
+                roles = _fin_roles(tickets, nt, nvb)
+                assert sorted(vb for vb, _ in roles if vb >= 0) == list(range(nvb))
+                assert [vb >= 0 for vb, _ in roles] == [i >= nt - nvb for i in range(nt)]
+                assert {t for vb, t in roles if vb >= 0} == {first + nt}
+                # the wait (counter >= target) ends exactly when the launch's last ticket is taken
+                assert [first + i >= first + nt for i in range(nt + 1)] == [False] * nt + [True]
