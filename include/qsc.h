@@ -38,6 +38,7 @@ extern "C" {
 
 #define QSC_OK 0
 #define QSC_EINVAL 100000
+#define QSC_EUNSUPPORTED 100001 /* configuration this library build does not run */
 #define QSC_MAX_BOUNDS 256 /* nbins <= 255: code 0xFF is the "unobserved" sentinel */
 #define QSC_MAX_R 16       /* rank bound of the fused passes */
 #define QSC_UNOBSERVED 0xFF
@@ -357,11 +358,15 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
 /* Fused S-step + next C-pass + that C-step's finish in ONE launch: qsc_scpass followed by
  * qsc_cfinish(mode 1) -- the same code, operands and summation order, so the same S, C,
  * moments, state and history bit for bit -- with the C-finish work items run by the last
- * R*nks + 2 workgroups to finish their tiles (they wait for the rest; no co-residency needed).
+ * R*nks + 2 workgroups to finish their tiles (they wait for the rest, holding their CUs: those
+ * R*nks + 2 workgroups must be co-resident).
  * A solver then runs  cpass, cfinish, scpass_fin x (n-1), spass: one launch per iteration.
  * Available when qsc_scpass_fin_supported(d, R): the fused launch at 16-wave workgroups with at
- * least R*nks + 2 tiles.  st->fused_fault is set (sticky) if a wait timed out; the caller must
- * then treat the run as invalid.  hist / hist_cap as qsc_cfinish. */
+ * least R*nks + 2 tiles, and R*nks + 2 plus a margin of 16 CUs for other streams within the
+ * device's CU count; the launch also checks the kernel instance's exact occupancy and returns
+ * QSC_EUNSUPPORTED when the late workgroups could not all be resident.  st->fused_fault is set
+ * (sticky) if a wait timed out anyway; the caller must then treat the run as invalid.
+ * hist / hist_cap as qsc_cfinish. */
 QSC_API int qsc_scpass_fin_supported(const qsc_obs_desc* d, int32_t R);
 QSC_API int qsc_scpass_fin(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
                            const int64_t* s_off, const void* c_entries, const int32_t* c_width,

@@ -20,6 +20,7 @@ QSC_MAX_R = 16
 QSC_SLICE = 32  # S-format slice (pixel positions per list group), include/qsc.h
 QSC_ENTRY_TAIL = 256  # pad entries after the last list (read-ahead tail), include/qsc.h
 QSC_EINVAL = 100000
+QSC_EUNSUPPORTED = 100001
 LOSSES = {"probit": 0, "squared": 1}  # QSC_LOSS_PROBIT, QSC_LOSS_SQUARED
 UNOBSERVED = 0xFF
 

@@ -457,6 +457,7 @@ QSC_API int qsc_rank_pad(int32_t R) {
 QSC_API const char* qsc_error_string(int code) {
   if (code == QSC_OK) return "success";
   if (code == QSC_EINVAL) return "invalid argument";
+  if (code == QSC_EUNSUPPORTED) return "configuration not supported by this build";
   return hipGetErrorString((hipError_t)code);
 }
 

@@ -1426,6 +1426,18 @@ struct FusedBlock {
       qsc_state *__restrict__ st, float *__restrict__ part_nll_s, float *__restrict__ part_nsq_s, \
       float *__restrict__ slab, float *__restrict__ part_nll_c, float *__restrict__ cnsq,         \
       AdamCache *__restrict__ acache, const int *__restrict__ c_split
+// scfin_kernel's form: C is written by its C-finish tail, so the kernel parameter carries no
+// __restrict__ (the tile body's restrict-qualified read-only view is scoped to scfused_tile,
+// which finishes every read of C before the tail writes it)
+#define QSC_SCFIN_KPARAMS                                                                      \
+  const E *__restrict__ s_ent, const int *__restrict__ s_width, const int64_t *__restrict__ s_off, \
+      const E *__restrict__ c_ent, const int *__restrict__ c_width,                                \
+      const int64_t *__restrict__ c_off, const int *__restrict__ c_kmap, int nks, int NP, int PT,  \
+      Lik lk, Edges E_, int nbins, int R, int K, float *__restrict__ S, float *C,                 \
+      float *__restrict__ mS, float *__restrict__ vS, qsc_adam ad, float lambda_s,                \
+      qsc_state *__restrict__ st, float *__restrict__ part_nll_s, float *__restrict__ part_nsq_s, \
+      float *__restrict__ slab, float *__restrict__ part_nll_c, float *__restrict__ cnsq,         \
+      AdamCache *__restrict__ acache, const int *__restrict__ c_split
 #define QSC_SCF_ARGS                                                                            \
   s_ent, s_width, s_off, c_ent, c_width, c_off, c_kmap, nks, NP, PT, lk, E_, nbins, R, K, S, C, mS, \
       vS, ad, lambda_s, st, part_nll_s, part_nsq_s, slab, part_nll_c, cnsq, acache, c_split
@@ -2031,17 +2043,19 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(QSC_CF_PARAMS) {
 // wait until every tile has arrived and then run the C-finish work items (cfinish_vb), the
 // earlier ones leave.  The C-step finish that was a launch of its own rides on the tail of the
 // fused launch: same code, operands and order as (qsc_scpass, qsc_cfinish mode 1), so the same
-// results bit for bit, one launch per iteration instead of two.  No co-residency is needed:
-// a waiting workgroup is one of the last R*nks + 2 to arrive, so at most R*nks + 1 others are
-// still to come, and the workgroups that already left free their CUs for them.  Tickets count
-// up for the life of the state (it is zeroed with it); launch j's arrivals hold tickets
-// [j*nt, (j+1)*nt).  A wait past kFinSpin polls (cannot happen unless the device is shared
-// with other work that holds every CU) sets the state's sticky fault word and skips the item.
+// results bit for bit, one launch per iteration instead of two.  Co-residency: a waiting
+// workgroup keeps its CU, and it is one of the last R*nks + 2 to arrive, so the waiters plus
+// the tiles still to arrive are at most R*nks + 2 workgroups that must be resident together;
+// the host checks that against the kernel's occupancy times the CU count, with a margin for
+// other streams (qsc_scpass_fin_supported, fin_fits), the workgroups that already left free
+// their CUs for the rest.  Tickets count up for the life of the state (it is zeroed with it);
+// launch j's arrivals hold tickets [j*nt, (j+1)*nt).  A wait past kFinSpin polls (other work
+// holding the CUs despite the check) sets the state's sticky fault word and skips the item.
 constexpr unsigned kFinSpin = 1u << 20;
 
 template <int RP, typename E, int KIND, bool LOG>
 __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
-    QSC_SCF_KPARAMS, float* Cw, float* __restrict__ mC, float* __restrict__ vC, qsc_adam adc,
+    QSC_SCFIN_KPARAMS, float* __restrict__ mC, float* __restrict__ vC, qsc_adam adc,
     float lambda_c, float* __restrict__ hist, int hist_cap, AdamCache* __restrict__ acache_c) {
   scfused_tile<RP, E, KIND, LOG>(QSC_SCF_ARGS, (int)blockIdx.x, (int)gridDim.x);
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -2080,7 +2094,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
   const int vb = *vbl;
   if (vb < 0) return;
   __threadfence();
-  cfinish_vb(vb, red, sc, sh3, slab, nt, nks, R, K, Cw, 1, nullptr, mC, vC, adc, lambda_c,
+  cfinish_vb(vb, red, sc, sh3, slab, nt, nks, R, K, C, 1, nullptr, mC, vC, adc, lambda_c,
              nullptr, cnsq, st, part_nll_c, nt * nks, part_nll_s, part_nsq_s,
              nt * PT / QSC_SLICE, hist, hist_cap, acache_c);
 }
@@ -2384,6 +2398,7 @@ int spass_bpc(int RP) { return RP > 8 ? 2 : RP == 8 ? QSC_SPASS_BPC8 : QSC_SPASS
   do {                                              \
     (void)kind;                                     \
     if (sr && RP == 8) LAUNCH(8, uint16_t, LIK_ONEBIT_SR, false); \
+    else return QSC_EUNSUPPORTED;                   \
   } while (0)
 #else
 #define QSC_DISPATCH_PASS(LAUNCH)                                                        \
@@ -2662,10 +2677,41 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
   return QSC_OK;
 }
 
+// CUs left to other streams (RCCL kernels, copies) when the fused-finish launch's late
+// workgroups must be co-resident
+constexpr int kFinCuMargin = 16;
+
+// the fused-finish launch's R*nks + 2 late workgroups fit on the device together: blocks per CU
+// of the exact kernel instance at its LDS size (cached per device, kernel and LDS size)
+static bool fin_fits(const void* kp, unsigned threads, size_t shm, int nvb) {
+  struct Key { int dev; const void* k; size_t shm; int cap; };
+  static Key cache[32];
+  static int ncache = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  int cap = -1;
+  for (int i = 0; i < ncache; ++i)
+    if (cache[i].dev == dev && cache[i].k == kp && cache[i].shm == shm) cap = cache[i].cap;
+  if (cap < 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kp, (int)threads, shm) != hipSuccess)
+      nb = 0;
+    cap = nb * cu_count();
+    if (ncache < 32) cache[ncache++] = Key{dev, kp, shm, cap};
+  }
+  return nvb + kFinCuMargin <= cap;
+}
+
 QSC_API int qsc_scpass_fin_supported(const qsc_obs_desc* d, int32_t R) {
   if (!qsc_scpass_supported(d, R)) return 0;
-  // the C-finish work items run on 16-wave workgroups, one item per late arrival
-  return (scpass_threads(d, R) == (unsigned)kFBlock && d->ntiles >= R * d->nks + 2) ? 1 : 0;
+  const int nvb = R * d->nks + 2;
+  // the C-finish work items run on 16-wave workgroups, one item per late arrival; the late
+  // arrivals must be co-resident (at least one 16-wave workgroup per CU; the launch itself
+  // checks the kernel instance's exact occupancy)
+  return (scpass_threads(d, R) == (unsigned)kFBlock && d->ntiles >= nvb &&
+          nvb + kFinCuMargin <= cu_count())
+             ? 1
+             : 0;
 }
 
 QSC_API int qsc_scpass_fin(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
@@ -2702,13 +2748,19 @@ QSC_API int qsc_scpass_fin(const qsc_obs_desc* d, const void* s_entries, const i
   hipStream_t s = STREAM(stream);
 #define SCFIN_LAUNCH(RPV, ET, KD, LG)                                                          \
   do {                                                                                         \
-    if constexpr (RPV <= 8)                                                                    \
+    if constexpr (RPV <= 8) {                                                                  \
+      if (!fin_fits(reinterpret_cast<const void*>(scfin_kernel<RPV, ET, KD, LG>), threads, shm, \
+                    R * d->nks + 2))                                                           \
+        return QSC_EUNSUPPORTED;                                                               \
       hipLaunchKernelGGL((scfin_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles),           \
                          dim3(threads), shm, s, (const ET*)s_entries, s_width, s_off,          \
                          (const ET*)c_entries, c_width, c_off, c_kmap, d->nks, NP, d->PT, lk,  \
                          E, d->nbins, R, d->K, S, C, mS, vS, ad, lambda_s, st, w.snll, w.snsq, \
-                         w.slab, w.cnll, w.cnsq, w.acache, (const int*)nullptr, C, mC, vC,     \
+                         w.slab, w.cnll, w.cnsq, w.acache, (const int*)nullptr, mC, vC,        \
                          adc, lambda_c, hist, hist_cap, w.acache + 2);                         \
+    } else {                                                                                   \
+      return QSC_EUNSUPPORTED;                                                                 \
+    }                                                                                          \
   } while (0)
   QSC_DISPATCH_PASS(SCFIN_LAUNCH);
 #undef SCFIN_LAUNCH

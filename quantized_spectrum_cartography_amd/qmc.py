@@ -302,6 +302,8 @@ class FreeSSolver:
         prepare_iterations(self, n)
 
     def run(self, n, use_graph=False):
+        """Enqueue n outer iterations (no host sync).  With `fin`, read results through
+        S_pixels() / history() or call check(): they raise if a fused-finish wait timed out."""
         run_iterations(self, n, use_graph)
 
     # ---- results --------------------------------------------------------------------------
@@ -309,6 +311,8 @@ class FreeSSolver:
         return self.engine.read_state()
 
     def S_pixels(self):
+        if self.fin:
+            self.check()  # one small readback: a timed-out C-finish wait leaves C incomplete
         return self.obs.to_pixels(self.S, self.R).reshape(self.R, 1, self.obs.I, self.obs.J)
 
     def check(self):

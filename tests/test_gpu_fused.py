@@ -503,9 +503,6 @@ def test_fused_finish_is_bitexact(n, shape):
     """qsc_scpass_fin (S-step + next C-pass + that C-step's finish in one launch, the finish on
     the last workgroups to arrive, include/qsc.h) gives the launch pairs' S, C, moments, costs
     and state bit for bit, eager and hipGraph."""
-    import os
-    if os.environ.get("QSC_FIN") != "1":
-        pytest.skip("the fused-finish launch is opt-in (QSC_FIN=1) until validated on MI355X")
     from quantized_spectrum_cartography_amd.obs import Observations
     from quantized_spectrum_cartography_amd.qmc import FreeSSolver
     R, I, J, K = shape
