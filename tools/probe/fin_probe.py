@@ -15,7 +15,7 @@ def main():
     I, J, K, R = (int(x) for x in (sys.argv[1:5] if len(sys.argv) > 4 else (192, 192, 256, 8)))
     n = int(sys.argv[5]) if len(sys.argv) > 5 else 3
     p = synthetic.onebit_problem(I, J, K, R, f=0.1, seed=5, keep_T=False)
-    o = Observations(p["Y"], p["Wx"], p["b"], p["sigma"], R_hint=R)
+    o = Observations(p["Y"], p["Wx"], p["b"], p["sigma"], R_hint=R, tile=1024)
     a = FreeSSolver(o, p["S0"], p["C0"], hist_cap=64, fin=False)
     b = FreeSSolver(o, p["S0"], p["C0"], hist_cap=64, fin=True)
     print("tiles", o.desc.ntiles, "fused finish applies", b.fin, flush=True)
