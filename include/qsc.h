@@ -417,6 +417,17 @@ QSC_API int qsc_supdate_slices(const qsc_obs_desc* d, int32_t R, int32_t s0, int
  * the updated shards so the pending S-update settles the global ||S_new||^2 on every rank. */
 QSC_API int qsc_slice_nsq(const qsc_obs_desc* d, int32_t R, const float* S, void* ws,
                           size_t ws_bytes, void* stream);
+/* qsc_cpass that also writes every position slice's ||S||^2 partial (the values qsc_slice_nsq
+ * writes, bit for bit) from the S tile it stages anyway: the K-slab solver's C-pass after the
+ * all-gather of S, which then needs no separate qsc_slice_nsq launch. */
+QSC_API int qsc_cpass_nsq(const qsc_obs_desc* d, const void* c_entries, const int32_t* c_width,
+                          const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
+                          int32_t R, const float* S, const float* C, void* ws, size_t ws_bytes,
+                          void* stream);
+/* byte offset, in the pass workspace, of the float where qsc_cpass / qsc_cpass_nsq leave ||C||^2
+ * of the C they read (the fixed order of qsc_sumsq_small): a K-slab solver all-reduces it in
+ * place and hands it to qsc_cfinish as normsq_c_ext.  -1 on an invalid descriptor. */
+QSC_API int64_t qsc_pass_cnsq_offset(const qsc_obs_desc* d, int32_t R);
 /* ||x||^2 into *out (fp32, fixed order), e.g. the local ||C_slab||^2 before an all-reduce */
 QSC_API int qsc_sumsq_small(const float* x, int32_t n, float* out, void* stream);
 /* debug builds (QSC_DEBUG=1, _build.py --debug): the source line of the last failed bounds

@@ -1245,7 +1245,7 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
     const int* __restrict__ kmap, int nks, int NP, int PT, Lik lk, Edges E_, int nbins, int R,
     int K,
     const float* __restrict__ S, const float* __restrict__ C, float* __restrict__ slab,
-    float* __restrict__ part_nll, float* __restrict__ cnsq) {
+    float* __restrict__ part_nll, float* __restrict__ cnsq, float* __restrict__ snsq_out) {
   using T = Ent<E>;
   using V4 = typename T::V4;
   constexpr int SP = TP<RP, KIND>::v;
@@ -1340,6 +1340,23 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
     if (u + NW < U) unit_begin(u + NW);
   }
   STAMP(wg, 2);
+
+  // 3b. (qsc_cpass_nsq, K-slab) every slice's ||S||^2 partial from the staged tile, in
+  //     slice_nsq_kernel's lane mapping (lane p + 32 h: position p, half row h) and order, so
+  //     the values are bit-identical to qsc_slice_nsq's / the shard updates' partials
+  if (snsq_out) {
+    constexpr int RH = RP / 2;
+    const int nsl = PT / QSC_SLICE, nt = gridDim.x;
+    const int p = lane & (QSC_SLICE - 1), h = lane >> 5;
+    for (int ls = w; ls < nsl; ls += NW) {
+      const float* row = Sl + (size_t)(ls * QSC_SLICE + p) * SP + h * RH;
+      float nsq = 0.0f;
+#pragma unroll
+      for (int j = 0; j < RH; ++j) nsq = __builtin_fmaf(row[j], row[j], nsq);
+      nsq = wave_sum(nsq);
+      if (lane == 0) snsq_out[tile_pos(t, ls * QSC_SLICE, nt) / QSC_SLICE] = nsq;
+    }
+  }
 
   // 4. fixed-order sum of the parts -> slab rows of this tile (NP > 1)
   if (NP > 1) {
@@ -2491,9 +2508,37 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
   return QSC_OK;
 }
 
+static int cpass_impl(const qsc_obs_desc* d, const void* c_entries, const int32_t* c_width,
+                      const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m, int32_t R,
+                      const float* S, const float* C, void* ws, size_t ws_bytes, void* stream,
+                      bool nsq);
+
 QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_t* c_width,
                       const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m, int32_t R,
                       const float* S, const float* C, void* ws, size_t ws_bytes, void* stream) {
+  return cpass_impl(d, c_entries, c_width, c_off, c_kmap, m, R, S, C, ws, ws_bytes, stream,
+                    false);
+}
+
+QSC_API int qsc_cpass_nsq(const qsc_obs_desc* d, const void* c_entries, const int32_t* c_width,
+                          const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
+                          int32_t R, const float* S, const float* C, void* ws, size_t ws_bytes,
+                          void* stream) {
+  return cpass_impl(d, c_entries, c_width, c_off, c_kmap, m, R, S, C, ws, ws_bytes, stream,
+                    true);
+}
+
+QSC_API int64_t qsc_pass_cnsq_offset(const qsc_obs_desc* d, int32_t R) {
+  if (!desc_ok(d) || R < 1 || R > QSC_MAX_R) return -1;
+  const uintptr_t base = 4096;  // any aligned address: the carve is base-relative
+  return (int64_t)(reinterpret_cast<uintptr_t>(carve(d, R, reinterpret_cast<void*>(base)).cnsq) -
+                   base);
+}
+
+static int cpass_impl(const qsc_obs_desc* d, const void* c_entries, const int32_t* c_width,
+                      const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m, int32_t R,
+                      const float* S, const float* C, void* ws, size_t ws_bytes, void* stream,
+                      bool nsq) {
   if (!desc_ok(d) || !m || m->nbounds - 1 != d->nbins || R < 1 || R > QSC_MAX_R || !S || !C ||
       !c_width || !c_off || !c_kmap || (d->c_entries > 0 && !c_entries) || !ws ||
       ws_bytes < ws_bytes_for(d, R))
@@ -2532,7 +2577,7 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
 #define CPASS_TILE_LAUNCH(RPV, ET, KD, LG)                                                     \
   hipLaunchKernelGGL((cpass_tile_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles), tb, tshm, \
                      s, (const ET*)c_entries, c_width, c_off, c_kmap, nks, NP, d->PT, lk, E,     \
-                     d->nbins, R, d->K, S, C, w.slab, w.cnll, w.cnsq)
+                     d->nbins, R, d->K, S, C, w.slab, w.cnll, w.cnsq, nsq ? w.snsq : nullptr)
       QSC_DISPATCH_PASS(CPASS_TILE_LAUNCH);
 #undef CPASS_TILE_LAUNCH
       QSC_CHECK_LAUNCH();
@@ -2549,6 +2594,7 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
   QSC_DISPATCH_PASS(CPASS_LAUNCH);
 #undef CPASS_LAUNCH
   QSC_CHECK_LAUNCH();
+  if (nsq) return qsc_slice_nsq(d, R, S, ws, ws_bytes, stream);  // (per-slice form: unfused)
   return QSC_OK;
 }
 

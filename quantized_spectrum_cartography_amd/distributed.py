@@ -13,16 +13,21 @@ One small collective per iteration; S never crosses the fabric.
 K-slab (the north-star layout): rank g owns the frequency bins [k0, k1) — its
 slab of the observations Y[k0:k1] and of the spectra C[:, k0:k1] — and a replica of S.  Per
 outer iteration
-  C-step: local C-pass; the non-squared regulariser lambda_c ||C||_F needs the GLOBAL ||C||^2,
-          so the ranks all-reduce one float before the fused cfinish (Adam + projection);
+  C-step: local C-pass (qsc_cpass_nsq: it also leaves the slab's ||C||^2 in its workspace and
+          rebuilds every slice's ||S||^2 partial from the S tile it stages); the non-squared
+          regulariser lambda_c ||C||_F needs the GLOBAL ||C||^2, so the ranks all-reduce that
+          one float in place before the fused cfinish (Adam + projection);
   S-step: local S-pass in gradient mode (partial dS over the slab's bins); a REDUCE-SCATTER of
           dS (Pp x RP fp32, 8.4 MB at 512x512, R = 8) leaves rank g the summed gradient of its
           1/N of the position slices; Adam on those rows only (qsc_supdate_slices: 1/N of the
           S/mS/vS traffic); an ALL-GATHER of the updated shards (in place in S) re-replicates S;
-          every rank then recomputes the per-slice ||S_new||^2 partials from the gathered S
-          (qsc_slice_nsq, bit-identical to the ones the shard updates produced), so the
-          regulariser norm of the next step is the same on all ranks without another collective.
+          the next C-pass rebuilds the per-slice ||S_new||^2 partials from the gathered S
+          (bit-identical to the ones the shard updates produced), so the regulariser norm of
+          the next step is the same on all ranks without another collective (before a final
+          flush, history() runs qsc_slice_nsq for the last iteration).
           Same bytes on the fabric as one all-reduce, 1/N of the Adam traffic per rank.
+An iteration is 4 kernels (cpass_nsq, cfinish, spass, supdate_slices) and 3 collectives
+(all-reduce of 1 float, reduce-scatter and all-gather of S-sized buffers).
 The next C-pass reads every tile's new S rows, which exist only after the all-gather, so the
 S update cannot be fused into it the way qsc_scpass fuses IJ-slab's.
 The pixel order of S (positions) is derived from the GLOBAL per-pixel observation counts
@@ -199,7 +204,9 @@ class KSlabSolver:
         self.C = C_init_local.detach().to(dev, torch.float32).reshape(R, obs.K).clone()
         self.mS, self.vS = torch.zeros_like(self.S), torch.zeros_like(self.S)
         self.mC, self.vC = torch.zeros_like(self.C), torch.zeros_like(self.C)
-        self.nsq_c = torch.zeros(1, dtype=torch.float32, device=dev)
+        # the C-pass's ||C_slab||^2 slot (all-reduced in place each C-step)
+        cn = getattr(engine, "cnsq", None)
+        self.nsq_c = cn() if cn is not None else torch.zeros(1, dtype=torch.float32, device=dev)
         self.adam_c = _lib.make_adam(lr_c, betas, eps, project_nonneg=project_c)
         self.adam_s = _lib.make_adam(lr_s, betas, eps, project_nonneg=False)
         self.lambda_c, self.lambda_s = float(lambda_c), float(lambda_s)
@@ -212,8 +219,7 @@ class KSlabSolver:
 
     def c_step(self):
         e = self.engine
-        e.cpass(self.S, self.C)
-        e.sumsq(self.C, self.nsq_c)
+        e.cpass_nsq(self.S, self.C)  # + ||C_slab||^2 into nsq_c, + the slices' ||S||^2
         self.dist.all_reduce(self.nsq_c)
         e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c,
                   normsq_ext=self.nsq_c)
@@ -227,7 +233,7 @@ class KSlabSolver:
                        self.r0, self.r1)
         lo = self.rank * self.chunk
         self.dist.all_gather_into_tensor(self.S_buf, self.S_buf[lo:lo + self.chunk])
-        e.slice_nsq(self.S)
+        # (the next cpass_nsq rebuilds every slice's ||S_new||^2 partial from the gathered S)
 
     def iteration(self):
         self.c_step()
@@ -267,6 +273,7 @@ class KSlabSolver:
     def history(self):
         """Global per-iteration costs (NLL columns summed over ranks; collective)."""
         e = self.engine
+        e.slice_nsq(self.S)  # the last S update's partials (no C-pass has run since)
         e.flush()
         st = e.read_state()
         n = min(int(st["iter"]), e.hist_cap)
@@ -274,9 +281,10 @@ class KSlabSolver:
         nll = h[:, :2].contiguous()
         self.dist.all_reduce(nll)
         h = torch.cat([nll, h[:, 2:]], dim=1).double().cpu()
-        e.sumsq(self.C, self.nsq_c)
-        self.dist.all_reduce(self.nsq_c)
-        nsq_c_final = float(self.nsq_c.item())
+        nsq = torch.zeros(1, dtype=torch.float32, device=self.C.device)
+        e.sumsq(self.C, nsq)
+        self.dist.all_reduce(nsq)
+        nsq_c_final = float(nsq.item())
         costs_c, costs_s = [], []
         for i in range(n):
             nll_c, nll_s, nsq_c, nsq_s = h[i].tolist()

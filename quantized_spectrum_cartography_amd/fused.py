@@ -58,6 +58,22 @@ class PassEngine:
                   _lib.ptr(o.c_kmap), o.model, self.R, _lib.ptr(S_pos), _lib.ptr(C),
                   _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
 
+    def cpass_nsq(self, S_pos, C):
+        """cpass that also writes every slice's ||S||^2 partial (qsc_cpass_nsq: the K-slab
+        C-pass after the all-gather of S, in place of a qsc_slice_nsq launch)."""
+        o = self.obs
+        _lib.call("qsc_cpass_nsq", self.desc, _lib.ptr(self.c_entries), _lib.ptr(o.c_width),
+                  _lib.ptr(o.c_off), _lib.ptr(o.c_kmap), o.model, self.R, _lib.ptr(S_pos),
+                  _lib.ptr(C), _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
+
+    def cnsq(self):
+        """A 1-float view of the workspace slot where the C-pass leaves ||C||^2 of the C it
+        read (qsc_pass_cnsq_offset): all-reduced in place by the K-slab solver."""
+        off = int(_lib.lib().qsc_pass_cnsq_offset(self.desc, self.R))
+        if off < 0 or off % 4:
+            raise _lib.QscError("qsc_pass_cnsq_offset failed")
+        return self.ws[off:off + 4].view(torch.float32)
+
     def cfinish(self, C, mode, dC=None, mC=None, vC=None, adam=None, lambda_c=0.0,
                 normsq_ext=None, record=True):
         hist, cap = (self.hist, self.hist_cap) if (record and self.hist_cap) else (None, 0)

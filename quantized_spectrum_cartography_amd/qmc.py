@@ -72,7 +72,7 @@ def _capture(solver, n, tolerant):
     solver is marked not capturable and runs eagerly from then on; otherwise the error is
     re-raised.  If the capture cannot be ended the error is always raised."""
     g = torch.cuda.CUDAGraph()
-    s = torch.cuda.Stream()
+    s = capture_stream()
     caller = torch.cuda.current_stream()
     s.wait_stream(caller)
     try:
@@ -114,6 +114,18 @@ def _hip_lib():
         h.hipGetLastError.restype = ctypes.c_int
         _hip = h
     return _hip
+
+
+def capture_stream():
+    """A side stream that is not in a capture: torch hands out streams from a fixed pool
+    (round robin), and a stream whose capture was invalidated stays invalidated for good
+    (abandon_capture), so after a failed capture the pool can return such a stream again;
+    skip those."""
+    for _ in range(4 * 32 + 1):  # torch's pool holds 32 streams per priority
+        s = torch.cuda.Stream()
+        if stream_capture_status(s) == 0:
+            return s
+    raise RuntimeError("no side stream out of capture for hipGraph capture")
 
 
 def stream_capture_status(stream):
@@ -239,11 +251,11 @@ class FreeSSolver:
             self._nmse_ws = torch.empty(_lib.lib().qsc_reduce_workspace_bytes(0),
                                         dtype=torch.uint8, device=self.S.device)
         # the fused body's C-step finish on the tail of its own launch (qsc_scpass_fin: one
-        # launch per iteration); not with per-iteration NMSE tracking, which runs between the
-        # S-step and that finish.  fin=None: opt-in through QSC_FIN=1 (off by default until the
-        # launch is validated on MI355X); fin=True/False forces it on/off
+        # launch per iteration, bit-exact with the launch pair); not with per-iteration NMSE
+        # tracking, which runs between the S-step and that finish.  fin=None: on where
+        # qsc_scpass_fin_supported (QSC_FIN=0 turns it off); fin=True/False forces it on/off
         if fin is None:
-            fin = os.environ.get("QSC_FIN", "0") == "1"
+            fin = os.environ.get("QSC_FIN", "1") != "0"
         self.fin = (self.fuse and bool(fin) and not self.nmse_every
                     and self.engine.scpass_fin_supported())
 

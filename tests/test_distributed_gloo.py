@@ -55,6 +55,7 @@ class _CpuEngine:
         self.hist = torch.zeros(4)
         self.st = dict(step_c=0, step_s=0, iter=0, normsq_s=0.0, nll_c=0.0, nll_s=0.0)
         self.calls = []
+        self._cnsq = torch.zeros(1)
 
     def _grad(self, S, C):
         """fp64 NLL, dS (position order, like S), dC"""
@@ -78,6 +79,16 @@ class _CpuEngine:
     def cpass(self, S, C):
         nll, _, dC = self._grad(S, C)
         self._dC, self.st["nll_c"] = torch.from_numpy(dC).float(), float(nll)
+
+    def cpass_nsq(self, S, C):
+        """qsc_cpass_nsq: the C-pass + ||C_slab||^2 into the cnsq slot + the slices' ||S||^2"""
+        self.calls.append("cpass_nsq")
+        self.cpass(S, C)
+        self._cnsq[0] = float((C.double() ** 2).sum())
+        self.st["normsq_s"] = float((S.double() ** 2).sum())  # (as slice_nsq)
+
+    def cnsq(self):
+        return self._cnsq
 
     def sumsq(self, x, out):
         out[0] = float((x.double() ** 2).sum())
@@ -137,6 +148,7 @@ class _CpuEngine:
 
     def slice_nsq(self, S):
         """qsc_slice_nsq: ||S||^2 of the all-gathered S (every rank the same)"""
+        self.calls.append("slice_nsq")
         self.st["normsq_s"] = float((S.double() ** 2).sum())
 
     def supdate(self, S, mS, vS, g, adam, lambda_s):
@@ -202,6 +214,8 @@ def _run(dist_mod, rank, world):
     sol.run(ITERS)
     # reduce-scatter -> Adam on the owned 1/N of S -> all-gather
     assert eng.calls.count("supdate_rows") == ITERS
+    # 4 kernels per iteration: the slices' ||S||^2 ride on the C-pass (no slice_nsq launch)
+    assert eng.calls.count("cpass_nsq") == ITERS and "slice_nsq" not in eng.calls[:-1]
     assert sol.r1 - sol.r0 <= -(-I * J // world)
     st = eng.read_state()
     st["shard"] = (sol.r0, sol.r1)

@@ -89,3 +89,26 @@ def test_adam_moments_flush_denormals_documented_deviation():
     torch.cuda.synchronize()
     assert torch.count_nonzero(mS).item() == 0 and torch.count_nonzero(vS).item() == 0
     assert torch.equal(S, S0)
+
+
+@pytest.mark.parametrize("R,tile", [(8, 512), (5, 512), (3, 256), (16, 512)])
+def test_cpass_nsq_writes_the_slice_partials(R, tile):
+    """qsc_cpass_nsq (the K-slab C-pass) leaves the workspace exactly as qsc_cpass followed by
+    qsc_slice_nsq does -- dC slab, NLL partials, ||C||^2 slot and every slice's ||S||^2
+    partial -- and the ||C||^2 slot (qsc_pass_cnsq_offset) holds qsc_sumsq_small's value."""
+    from quantized_spectrum_cartography_amd.fused import PassEngine
+    from quantized_spectrum_cartography_amd.obs import Observations
+    d = _random_case(94 + R, R, 64, 80, 96)
+    obs = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=R, tile=tile)
+    S = obs.to_positions(d["S0"].reshape(R, -1))
+    C = d["C0"].reshape(R, -1).cuda().contiguous()
+    a, b = PassEngine(obs, R), PassEngine(obs, R)
+    a.cpass(S, C)
+    a.slice_nsq(S)
+    b.cpass_nsq(S, C)
+    torch.cuda.synchronize()
+    assert torch.equal(a.ws, b.ws)
+    ref = torch.zeros(1, device="cuda")
+    a.sumsq(C, ref)
+    torch.cuda.synchronize()
+    assert torch.equal(b.cnsq(), ref)
