@@ -16,9 +16,11 @@ from . import reference_ops as ro
 
 def free_s_solve(S0, C0, Y, Wx, b, sigma, offset=0.0, log_model=False, n_iter=10,
                  lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2, snapshots=(), timer=None,
-                 loss="probit"):
+                 loss="probit", project_s=False):
     """loss="squared": the Euclidean criterion of qmc/qmc_dowjons.ipynb :138-162 in place of
-    the probit likelihood (Obs = mid_bin(Y, b), computed once as at :114)."""
+    the probit likelihood (Obs = mid_bin(Y, b), computed once as at :114).
+    project_s: S[S<0] = 0 after each S-step (the C-step's projection form, :579), the build's
+    S >= 0 option for free S under the log model (not a reference setting)."""
     if loss == "squared":
         Obs = ro.mid_bin(Y, b)
 
@@ -49,6 +51,9 @@ def free_s_solve(S0, C0, Y, Wx, b, sigma, offset=0.0, log_model=False, n_iter=10
         cost = nll + lambda_c * torch.norm(C, "fro") + lambda_s * torch.norm(S, "fro")
         cost.backward()
         optS.step()
+        if project_s:
+            with torch.no_grad():
+                S[S < 0] = 0
         costs_s.append(cost.item())
         t2 = time.perf_counter()
         step_times.append((t1 - t0, t2 - t1))

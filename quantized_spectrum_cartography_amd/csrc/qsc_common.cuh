@@ -652,11 +652,13 @@ __device__ __forceinline__ void adam_elem_fast(float& p, float& m, float& v, flo
 // Adam of the fused S-pass epilogue and of qsc_supdate), with the S regulariser folded in:
 // g = a + p * coef.  Per element the same operations in the same order as adam_elem_fast (the
 // bc2_sqrt reciprocal is the one div_fix forms), so the results are bitwise those of the scalar
-// form.  Returns sum_j p_new[j]^2 accumulated in j order.
+// form.  proj: the projection onto S >= 0 after the step (qsc_adam::project_nonneg, the
+// reference's C[C<0] = 0 form: -0 stays -0), before the norm.  Returns sum_j p_new[j]^2
+// accumulated in j order.
 template <int RH>
 __device__ __forceinline__ float adam_row_fast(float (&p)[RH], float (&m)[RH], float (&v)[RH],
                                                const float (&a)[RH], float coef,
-                                               const AdamScalars& s) {
+                                               const AdamScalars& s, bool proj) {
   float nsq = 0.0f;
 #pragma unroll
   for (int j = 0; j < RH; j += 2) {
@@ -681,8 +683,8 @@ __device__ __forceinline__ float adam_row_fast(float (&p)[RH], float (&m)[RH], f
     const f2v q2 = x * ry;
     const f2v r2 = fma2(-q2, den, x);
     const f2v pn = pp + fma2(r2, ry, q2);
-    p[j] = pn.x;
-    p[j + 1] = pn.y;
+    p[j] = (proj && pn.x < 0.0f) ? 0.0f : pn.x;
+    p[j + 1] = (proj && pn.y < 0.0f) ? 0.0f : pn.y;
     m[j] = mm.x;
     m[j + 1] = mm.y;
     v[j] = vv.x;

@@ -1071,7 +1071,7 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
         m[j] = c.mv[j];
         v[j] = c.vv[j];
       }
-      float nsq = adam_row_fast<RH>(pv, m, v, a, sc.coef, sc.as);
+      float nsq = adam_row_fast<RH>(pv, m, v, a, sc.coef, sc.as, ad.project_nonneg != 0);
       st_row<RH>(S + blk, ln.half, pv);
       st_row<RH>(mS + blk, ln.half, m);
       st_row<RH>(vS + blk, ln.half, v);
@@ -1685,7 +1685,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
       m[j] = c.mv[j];
       v[j] = c.vv[j];
     }
-    float nsq = adam_row_fast<RH>(pv, m, v, a, sc.coef, sc.as);
+    float nsq = adam_row_fast<RH>(pv, m, v, a, sc.coef, sc.as, ad.project_nonneg != 0);
     const int64_t blk = (int64_t)s * QSC_SLICE * RP;  // the slice's rows (uniform)
     st_row<RH>(S + blk, ln.half, pv);
     st_row<RH>(mS + blk, ln.half, m);
@@ -2086,17 +2086,23 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
   // the state, and must stay aligned to launches, so it may never wrap)
   unsigned long long* ticket = reinterpret_cast<unsigned long long*>(st) + 5;
   int* fault = reinterpret_cast<int*>(st) + 9;              // qsc_state.fused_fault
-  __threadfence();
+  // Fences, chosen for the 8 non-coherent XCD L2s: the workgroup barrier orders every thread's
+  // tile writes before thread 0's ONE agent-scope release fence (an L2 write-back, no
+  // invalidate), then a relaxed ticket increment.  Waiters poll with relaxed agent-scope loads
+  // (L2-bypassing, no invalidate: an acquire load per poll would invalidate this XCD's L2 under
+  // the workgroups still running there, measured 160 us per launch instead of ~34) and take
+  // one acquire fence after the wait.
   __syncthreads();
   if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const unsigned long long tk =
-        __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long a = tk % (unsigned long long)nt;
     int vb = (int)a - (nt - nvb);
     if (vb >= 0) {
       const unsigned long long target = tk - a + (unsigned long long)nt;
       unsigned polls = 0;
-      while (__hip_atomic_load(ticket, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      while (__hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         if (++polls > kFinSpin) {
           __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           vb = -1;
@@ -2104,13 +2110,13 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
         }
         __builtin_amdgcn_s_sleep(2);
       }
+      if (vb >= 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     *vbl = vb;
   }
   __syncthreads();
   const int vb = *vbl;
   if (vb < 0) return;
-  __threadfence();
   cfinish_vb(vb, red, sc, sh3, slab, nt, nks, R, K, C, 1, nullptr, mC, vC, adc, lambda_c,
              nullptr, cnsq, st, part_nll_c, nt * nks, part_nll_s, part_nsq_s,
              nt * PT / QSC_SLICE, hist, hist_cap, acache_c);
@@ -2190,7 +2196,7 @@ __global__ void __launch_bounds__(kSBlock) supdate_kernel(
   ld_row<RH>(vS + o, v);
   ld_row<RH>(gsrc + o, g);
   // the fused S-pass's update (no projection)
-  float nsq = adam_row_fast<RH>(p, m, v, g, sc.coef, sc.as);
+  float nsq = adam_row_fast<RH>(p, m, v, g, sc.coef, sc.as, ad.project_nonneg != 0);
   st_row<RH>(S + o, p);
   st_row<RH>(mS + o, m);
   st_row<RH>(vS + o, v);
@@ -2226,7 +2232,7 @@ __global__ void __launch_bounds__(kSBlock) supdate_slices_kernel(
   ld_row<RH>(mS + o, m);
   ld_row<RH>(vS + o, v);
   ld_row<RH>(g_own + og, g);
-  float nsq = adam_row_fast<RH>(p, m, v, g, sc.coef, sc.as);
+  float nsq = adam_row_fast<RH>(p, m, v, g, sc.coef, sc.as, ad.project_nonneg != 0);
   st_row<RH>(S + o, p);
   st_row<RH>(mS + o, m);
   st_row<RH>(vS + o, v);

@@ -224,7 +224,7 @@ class FreeSSolver:
 
     def __init__(self, obs, S_init, C_init, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
                  betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024, fuse=True,
-                 T_true=None, nmse_every=0, fin=None):
+                 T_true=None, nmse_every=0, fin=None, project_s=False):
         self.obs = obs
         R = S_init.shape[0]
         self.R = R
@@ -234,7 +234,10 @@ class FreeSSolver:
         self.mS, self.vS = torch.zeros_like(self.S), torch.zeros_like(self.S)
         self.mC, self.vC = torch.zeros_like(self.C), torch.zeros_like(self.C)
         self.adam_c = _lib.make_adam(lr_c, betas, eps, project_nonneg=project_c)
-        self.adam_s = _lib.make_adam(lr_s, betas, eps, project_nonneg=False)
+        # project_s: S >= 0 after every S-step (S[S<0] = 0, fused into the S-side Adam), the
+        # domain of the reference's generator / decoder S (sigmoid outputs, deep_prior/networks/
+        # dip.py:80); for free S under the log model, where T_hat + offset must stay > 0
+        self.adam_s = _lib.make_adam(lr_s, betas, eps, project_nonneg=project_s)
         self.lambda_c, self.lambda_s = float(lambda_c), float(lambda_s)
         self.engine.init_state(self.S)
         self.fuse = bool(fuse) and self.engine.scpass_supported()
@@ -355,7 +358,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
           betas=(0.9, 0.999), eps=1e-8, project_c=True, generator=None, Z_init=None,
           restart=False, restart_samples=(200, 200), T_true=None, nmse_every=0,
           use_graph=False, obs=None, tile=None, callback=None, loss="probit", fuse=True,
-          fin=None):
+          fin=None, project_s=False):
     """Alternating S/C probit-MLE (qmc/qmc.ipynb :559-645).
 
     Args mirror the notebook globals: Y (K,1,I,J) bin indices, Wx (K,1,I,J) 0/1 mask,
@@ -365,6 +368,8 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
     loss="squared" replaces the probit likelihood by the Euclidean criterion
     ||Wx (T_hat - Obs)||_F^2 of qmc/qmc_dowjons.ipynb :142-162 (Obs = bin midpoints,
     get_quantized_obs_from_ordinal); the cost history then holds that criterion.
+    project_s=True keeps free S >= 0 (S[S<0] = 0 after each S-step, as C at :579): the log
+    model needs T_hat + offset > 0, which free S can otherwise leave.
     Returns a SolveResult with S (R,1,I,J) and C (R,K) on the GPU.
     """
     if log_model and obs is None:
@@ -390,7 +395,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
         sol = FreeSSolver(obs, S_init, C_init, lambda_c, lambda_s, lr_c, lr_s, betas, eps,
                           project_c, hist_cap=max_iter, fuse=fuse,
                           T_true=T_true if nmse_every else None, nmse_every=nmse_every,
-                          fin=fin)
+                          fin=fin, project_s=project_s)
         done = 0
         chunk = nmse_every if (callback is not None and nmse_every) else max_iter
         while done < max_iter:

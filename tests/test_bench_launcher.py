@@ -86,3 +86,32 @@ def test_heartbeat_reports_long_phases(capsys):
     with bench.heartbeat(1, "phase", every=0.05):  # other ranks stay quiet
         time.sleep(0.12)
     assert capsys.readouterr().err == ""
+
+
+def test_multi_gpu_default_is_the_metric():
+    """BASELINE.json's metric is the ONE fixed 512x512x256 R=8 map at 1/2/4/8 GPUs, split by the
+    north-star K-slab layout: --gpus N defaults to strong scaling, K-slab, config c3; the other
+    layout and weak scaling ride along as extra keys."""
+    a = _args(["--gpus", "8"])
+    assert a.scaling == "strong" and a.shard == "kslab" and a.config == "c3"
+    assert not a.no_extra
+
+
+def test_extra_measurement_plan(monkeypatch):
+    """The extra keys of an N > 1 run: the other layout at the same scaling, plus weak IJ-slab;
+    weak values count every rank's grad-steps, strong ones the fixed map's."""
+    built = []
+
+    class _Obs:
+        nnz = 7
+
+    def fake_build(cfg, scaling, shard, rank, world, dist, hist_cap, keep_inputs=False):
+        built.append((scaling, shard))
+        return {}, _Obs(), object()
+
+    monkeypatch.setattr(bench, "build_solver", fake_build)
+    monkeypatch.setattr(bench, "timed_run", lambda *a, **k: (2.0, 2.0))
+    a = _args(["--gpus", "4", "--steps", "10"])
+    out = bench.extra_measurements((8, 8, 8, 2), a, 1, 4, None, "strong", "kslab")
+    assert built == [("strong", "ijslab"), ("weak", "ijslab")]
+    assert out["layouts"]["ijslab"]["value"] == 5.0 and out["weak"]["ijslab"]["value"] == 20.0

@@ -522,3 +522,29 @@ def test_fused_finish_is_bitexact(n, shape):
         st, rs = sol.state(), ref.state()
         assert st["fused_fault"] == 0
         assert st == rs
+
+
+@pytest.mark.parametrize("log_model,R,I,J,K,s_scale,lr_s,n", [
+    (True, 4, 32, 32, 16, None, 0.1, 3),        # log model: 0.5 % of S projected
+    (False, 8, 64, 64, 256, 0.02, 0.05, 6)])   # one-bit, fused launches
+def test_project_s_matches_reference_op_sequence(log_model, R, I, J, K, s_scale, lr_s, n):
+    """project_s (S[S<0] = 0 after each S-step, fused into the S-side Adam of the pass kernels;
+    the log model's S >= 0 domain) vs the oracle's op sequence with the same projection, on a
+    start where the unprojected S goes negative -- through the fused launches (fin included)
+    for the one-bit case, the three-launch form for the log model."""
+    from quantized_spectrum_cartography_amd import qmc
+    d = _random_case(61, R, I, J, K, f=0.3, log_model=log_model)
+    S0 = d["S0"] if s_scale is None else \
+        s_scale * torch.rand(R, 1, I, J, generator=torch.Generator().manual_seed(5))
+    kw = dict(offset=d["offset"], log_model=log_model, lr_s=lr_s)
+    free = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], S_init=S0, C_init=d["C0"],
+                     max_iter=n, **kw)
+    assert bool((free.S < 0).any()), "the case must drive some of S below 0"
+    res = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], S_init=S0, C_init=d["C0"],
+                    max_iter=n, project_s=True, **kw)
+    assert bool((res.S >= 0).all()) and bool((res.S == 0).any())
+    ref = osolver.free_s_solve(S0, d["C0"], d["Y"], d["Wx"], d["b"], d["sigma"],
+                               offset=d["offset"], log_model=log_model, n_iter=n, lr_s=lr_s,
+                               project_s=True)
+    assert rel_fro(res.S.cpu().numpy(), ref["S"].numpy()) < 1e-5
+    assert rel_fro(res.C.cpu().numpy(), ref["C"].numpy()) < 1e-5
