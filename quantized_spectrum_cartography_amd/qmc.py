@@ -255,10 +255,11 @@ class FreeSSolver:
                                         dtype=torch.uint8, device=self.S.device)
         # the fused body's C-step finish on the tail of its own launch (qsc_scpass_fin: one
         # launch per iteration, bit-exact with the launch pair); not with per-iteration NMSE
-        # tracking, which runs between the S-step and that finish.  fin=None: on where
-        # qsc_scpass_fin_supported (QSC_FIN=0 turns it off); fin=True/False forces it on/off
+        # tracking, which runs between the S-step and that finish.  fin=None: off unless QSC_FIN=1
+        # (measured on MI355X at C3: 40.3 us for the one launch against 30.6 + 3.2 us for the
+        # launch pair, profiles/r04); fin=True/False forces it on/off where supported
         if fin is None:
-            fin = os.environ.get("QSC_FIN", "1") != "0"
+            fin = os.environ.get("QSC_FIN", "0") == "1"
         self.fin = (self.fuse and bool(fin) and not self.nmse_every
                     and self.engine.scpass_fin_supported())
 
