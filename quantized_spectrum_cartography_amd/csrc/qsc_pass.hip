@@ -909,8 +909,13 @@ __device__ __forceinline__ void slice_load(SliceIn<RP, E, ADAM>& in, const E* __
                                            const float* __restrict__ mS,
                                            const float* __restrict__ vS) {
   using V2 = typename Ent<E>::V2;
-  in.j1 = width[s] >> 2;
-  in.src = reinterpret_cast<const V2*>(ent + off[s]);
+  // both slice words read before either is used: one scalar-cache round trip, not two in a
+  // chain (the entry reads below depend on both; at the start of a launch this chain is the
+  // critical path to the first slice's data)
+  const int64_t o = off[s];
+  const int wd = width[s];
+  in.j1 = wd >> 2;
+  in.src = reinterpret_cast<const V2*>(ent + o);
   const int jlast = max(in.j1 - 1, 0);
 #pragma unroll
   for (int i = 0; i < kGroupS; ++i)
@@ -1416,6 +1421,20 @@ size_t cpass_tile_lds(int PT, int R, int nks, int NP, bool sr) {
 // ---------------------------------------------------------------------------------------
 // fused launch block: 16 waves (4 per SIMD, 128 VGPRs) up to rank 8; 8 waves at rank 16, whose
 // two slice register sets and 16-float rows need up to 256 VGPRs (2 waves per SIMD)
+// Stores of the values the fused finish's tail reads (qsc_scpass_fin: dC slab rows, NLL / norm
+// partials, the state's book-keeping fields): with FIN they are agent-scope relaxed atomic
+// stores, i.e. written through this XCD's L2 to the device coherence point, so that the
+// finishing workgroups on other XCDs see them once the stores have completed (s_waitcnt) --
+// no L2 write-back fence per workgroup (measured: with one `buffer_wbl2` per workgroup the
+// launch took 40 us against 31 + 3 for the launch pair).  Without FIN: plain stores.
+template <bool FIN, typename T>
+__device__ __forceinline__ void st_fin(T* p, T v) {
+  if constexpr (FIN)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+
 template <int RP>
 struct FusedBlock {
   static constexpr int v = RP > 8 ? 512 : 64 * QSC_FUSED_WAVES;
@@ -1461,7 +1480,7 @@ struct FusedBlock {
 
 // One pixel tile t of nt of the fused launch (scfused_kernel, scfin_kernel: t = the workgroup).
 // C is read-only here; scfin_kernel's C-finish writes it after every tile has finished.
-template <int RP, typename E, int KIND, bool LOG>
+template <int RP, typename E, int KIND, bool LOG, bool FIN = false>
 __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const int nt) {
   using V4 = typename Ent<E>::V4;
   constexpr int CP = TP<RP, KIND>::v;  // C^T row pitch == S tile row pitch
@@ -1608,11 +1627,11 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
       if (t == 0) {
         // book-keeping of spass_kernel (mode 1)
         int pend = st->pending;
-        if (pend & QSC_PEND_C) st->step_c += 1;
+        if (pend & QSC_PEND_C) st_fin<FIN>(&st->step_c, st->step_c + 1);
         pend &= ~QSC_PEND_C;
-        st->pending = pend | QSC_PEND_SNLL | QSC_PEND_SUPD;
-        st->normsq_s_prev = nsq_s;
-        st->iter += 1;
+        st_fin<FIN>(&st->pending, pend | QSC_PEND_SNLL | QSC_PEND_SUPD);
+        st_fin<FIN>(&st->normsq_s_prev, nsq_s);
+        st_fin<FIN>(&st->iter, st->iter + 1);
       }
     }
     STAMP(wg, 11);  // (wave 0: the scalars are set)
@@ -1638,7 +1657,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
         s2 = __builtin_fmaf(c, c, s2);
       }
     const float nsq = block_sum(s2, Nl);
-    if (threadIdx.x == 0) *cnsq = nsq;
+    if (threadIdx.x == 0) st_fin<FIN>(cnsq, nsq);
   }
 
   // 2. S-step over the wave's slices (next slice's reads in flight; the two register sets
@@ -1698,9 +1717,9 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
       st_row<RH>(Sl + (sr_off(PT) + il * QSC_SLICE + p) * CP + h * RH, nv);
     }
     nsq = wave_sum_dpp(nsq);
-    if (lane == 0) part_nsq_s[s] = nsq;
+    if (lane == 0) st_fin<FIN>(&part_nsq_s[s], nsq);
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
-    if (lane == 0) part_nll_s[s] = nll_w;
+    if (lane == 0) st_fin<FIN>(&part_nll_s[s], nll_w);
     STAMP(wg, 5 + min(n, 8));  // end of the wave's n-th slice
     il = il1;
     ++n;
@@ -1813,10 +1832,10 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     if (NP == 1) {
 #pragma unroll
       for (int j = 0; j < RP / 2; ++j) {
-        if (2 * j < R) slab[((int64_t)t * R + 2 * j) * Kp + k] = accp[j].x;
-        if (2 * j + 1 < R) slab[((int64_t)t * R + 2 * j + 1) * Kp + k] = accp[j].y;
+        if (2 * j < R) st_fin<FIN>(&slab[((int64_t)t * R + 2 * j) * Kp + k], accp[j].x);
+        if (2 * j + 1 < R) st_fin<FIN>(&slab[((int64_t)t * R + 2 * j + 1) * Kp + k], accp[j].y);
       }
-      if (lane == 0) part_nll_c[wi] = nll_w;
+      if (lane == 0) st_fin<FIN>(&part_nll_c[wi], nll_w);
     } else {
       to_pl(accp);
       if (lane == 0) Nl[u] = nll_w;
@@ -1837,12 +1856,12 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
 #else
       const int kk = c_kmap[((int64_t)t * nks + ks) * 64 + l];
 #endif
-      slab[((int64_t)t * R + r) * Kp + kk] = acc;
+      st_fin<FIN>(&slab[((int64_t)t * R + r) * Kp + kk], acc);
     }
     for (int ks = threadIdx.x; ks < nks; ks += blockDim.x) {
       float acc = Nl[ks * NP];
       for (int pp = 1; pp < NP; ++pp) acc += Nl[ks * NP + pp];
-      part_nll_c[t * nks + ks] = acc;
+      st_fin<FIN>(&part_nll_c[t * nks + ks], acc);
     }
   }
   STAMP(wg, kStampLast);
@@ -2074,7 +2093,7 @@ template <int RP, typename E, int KIND, bool LOG>
 __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
     QSC_SCFIN_KPARAMS, float* __restrict__ mC, float* __restrict__ vC, qsc_adam adc,
     float lambda_c, float* __restrict__ hist, int hist_cap, AdamCache* __restrict__ acache_c) {
-  scfused_tile<RP, E, KIND, LOG>(QSC_SCF_ARGS, (int)blockIdx.x, (int)gridDim.x);
+  scfused_tile<RP, E, KIND, LOG, true>(QSC_SCF_ARGS, (int)blockIdx.x, (int)gridDim.x);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int nt = gridDim.x, nvb = R * nks + 2;
   // C-finish scratch and the arrival broadcast word, over the (now idle) tile LDS
@@ -2086,19 +2105,26 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
   // the state, and must stay aligned to launches, so it may never wrap)
   unsigned long long* ticket = reinterpret_cast<unsigned long long*>(st) + 5;
   int* fault = reinterpret_cast<int*>(st) + 9;              // qsc_state.fused_fault
-  // Fences, chosen for the 8 non-coherent XCD L2s: the workgroup barrier orders every thread's
-  // tile writes before thread 0's ONE agent-scope release fence (an L2 write-back, no
-  // invalidate), then a relaxed ticket increment.  Waiters poll with relaxed agent-scope loads
+  // Ordering, chosen for the 8 non-coherent XCD L2s: everything the C-finish items read was
+  // stored write-through at agent scope by the tile body (st_fin), so each wave waits for its
+  // own stores to complete (vmcnt 0: at the device coherence point), the workgroup barrier
+  // joins the waves, and thread 0 takes its ticket with a relaxed agent-scope increment -- no
+  // release fence, whose L2 write-back per workgroup (while 25 MB of S-step writes stream
+  // through the L2s) cost ~6 us per launch.  Waiters poll with relaxed agent-scope loads
   // (L2-bypassing, no invalidate: an acquire load per poll would invalidate this XCD's L2 under
   // the workgroups still running there, measured 160 us per launch instead of ~34) and take
-  // one acquire fence after the wait.
+  // one acquire fence after the wait (the state line may sit stale in this XCD's L2).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const unsigned long long tk =
         __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long a = tk % (unsigned long long)nt;
     int vb = (int)a - (nt - nvb);
+#if QSC_DIAG_STAMPS
+    g_stamps[(int)blockIdx.x * (FusedBlock<RP>::v / 64) * kStamps + 19] = __builtin_amdgcn_s_memtime();
+    g_stamps[(int)blockIdx.x * (FusedBlock<RP>::v / 64) * kStamps + 18] = (unsigned long long)a;
+#endif
     if (vb >= 0) {
       const unsigned long long target = tk - a + (unsigned long long)nt;
       unsigned polls = 0;
@@ -2114,12 +2140,15 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
     }
     *vbl = vb;
   }
+  [[maybe_unused]] const int wg = (int)blockIdx.x * (FusedBlock<RP>::v / 64) + (threadIdx.x >> 6);
+  STAMP(wg, 20);  // (diagnostic builds) wave 0: ticket taken and, for a waiter, the wait over
   __syncthreads();
   const int vb = *vbl;
   if (vb < 0) return;
   cfinish_vb(vb, red, sc, sh3, slab, nt, nks, R, K, C, 1, nullptr, mC, vC, adc, lambda_c,
              nullptr, cnsq, st, part_nll_c, nt * nks, part_nll_s, part_nsq_s,
              nt * PT / QSC_SLICE, hist, hist_cap, acache_c);
+  STAMP(wg, 21);  // C-finish item done
 }
 
 // ---------------------------------------------------------------------------------------

@@ -13,7 +13,31 @@ import torch
 from . import _model
 
 
-def onebit_problem(I, J, K, R, f=0.1, seed=20260, device="cuda", keep_T=True):
+def onebit_problem(I, J, K, R, f=0.1, seed=20260, device="cuda", keep_T=True, device_rng=False):
+    """device_rng=True draws the same recipe from a device generator (seeded with `seed`): the
+    same problem on every rank of a job, without the host RNG's minutes for C4-sized maps
+    (512 x 512 x 1024: 268 M noise and mask samples), but not the host draw's values."""
+    if device_rng:
+        g = torch.Generator(device=device).manual_seed(seed)
+        S_true = torch.rand(R, 1, I, J, generator=g, device=device)
+        C_true = torch.rand(R, K, generator=g, device=device)
+        T_true = _model.get_tensor(S_true, C_true)
+        thr = float(T_true.median())
+        tmax, tmin = float(T_true.max()), float(T_true.min())
+        sigma = (tmax - tmin) / 4
+        b = torch.tensor([0.0, thr, tmax])
+        noise = torch.randn(T_true.shape, generator=g, device=device)
+        Y = _model.quantize(T_true, sigma, b, noise=noise).unsqueeze(1)
+        del noise
+        Wx = torch.bernoulli(torch.full((K, 1, I, J), f, device=device), generator=g)
+        S0 = 0.5 * torch.rand(R, 1, I, J, generator=g, device=device)
+        C0 = 0.5 * torch.rand(R, K, generator=g, device=device)
+        S_true, C_true, S0, C0 = S_true.cpu(), C_true.cpu(), S0.cpu(), C0.cpu()
+        out = dict(S_true=S_true, C_true=C_true, b=b, sigma=sigma, Y=Y, Wx=Wx, S0=S0, C0=C0,
+                   log_model=False, offset=0.0, thr=thr)
+        if keep_T:
+            out["T_true"] = T_true
+        return out
     g_state = torch.random.get_rng_state()
     try:
         torch.manual_seed(seed)
