@@ -107,7 +107,8 @@ typedef struct qsc_state {
   int32_t fused_fault; /* sticky: 1 after a qsc_scpass_fin launch whose C-finish wait timed
                           out (the launch's C update is then incomplete: results invalid) */
   uint64_t fin_ticket; /* qsc_scpass_fin arrival counter, never wraps (zeroed by qsc_state_init) */
-  float reserved[4];
+  uint64_t fin_done;   /* qsc_scpass_loop: C-finish work items completed, never wraps (zeroed) */
+  float reserved[2];
 } qsc_state;
 
 /* Packed observation layout, produced by qsc_obs_layout (host struct).
@@ -375,6 +376,38 @@ QSC_API int qsc_scpass_fin(const qsc_obs_desc* d, const void* s_entries, const i
                            const qsc_adam* adam_s, float lambda_s, float* mC, float* vC,
                            const qsc_adam* adam_c, float lambda_c, qsc_state* st, float* hist,
                            int32_t hist_cap, void* ws, size_t ws_bytes, void* stream);
+/* n_iter fused bodies (qsc_scpass_fin, same results bit for bit) in ONE persistent launch: one
+ * 16-wave workgroup per tile for the whole launch; after each body's C-finish every workgroup
+ * waits (st->fin_done) for that iteration's R*nks + 2 finish items before the next body, so
+ * all tiles must be resident at once: qsc_scpass_loop_supported(d, R) requires the fused
+ * finish and ntiles <= the device's CU count, and the launch checks the kernel instance's
+ * occupancy (QSC_EUNSUPPORTED otherwise).  Nothing else may hold the device's CUs while it
+ * runs (a wait past ~10^6 polls sets st->fused_fault and ends the launch: results invalid).
+ * A solver then runs  cpass, cfinish, scpass_loop(n-1), spass: two short launches and one
+ * persistent one per solve.  hist / hist_cap as qsc_cfinish.  Replaces the same notebook steps
+ * as qsc_scpass_fin (qmc/qmc.ipynb :562-634, the S-step and the next C-step, n-1 times). */
+QSC_API int qsc_scpass_loop_supported(const qsc_obs_desc* d, int32_t R);
+QSC_API int qsc_scpass_loop(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
+                            const int64_t* s_off, const void* c_entries, const int32_t* c_width,
+                            const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
+                            int32_t R, float* S, float* C, float* mS, float* vS,
+                            const qsc_adam* adam_s, float lambda_s, float* mC, float* vC,
+                            const qsc_adam* adam_c, float lambda_c, qsc_state* st, float* hist,
+                            int32_t hist_cap, int32_t n_iter, void* ws, size_t ws_bytes,
+                            void* stream);
+/* qsc_scpass_loop with a diagnostics array: progress[t] (ntiles int32, device) receives
+ * 16 * iteration + the phase workgroup t last reached (1 tile body, 2 ticket, 3 wait over,
+ * 4 C-finish item done, 5 next-iteration wait over; 9 / 10 the ticket / fin_done wait timed
+ * out). */
+QSC_API int qsc_scpass_loop_dbg(const qsc_obs_desc* d, const void* s_entries,
+                                const int32_t* s_width, const int64_t* s_off,
+                                const void* c_entries, const int32_t* c_width,
+                                const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
+                                int32_t R, float* S, float* C, float* mS, float* vS,
+                                const qsc_adam* adam_s, float lambda_s, float* mC, float* vC,
+                                const qsc_adam* adam_c, float lambda_c, qsc_state* st,
+                                float* hist, int32_t hist_cap, int32_t n_iter, int32_t* progress,
+                                void* ws, size_t ws_bytes, void* stream);
 /* reduce the C-pass slab (fixed order).  mode 0: write dC (NLL gradient only); mode 1: fused
  * C-step: dC + lambda_c*C/||C||, Adam on C, projection; mode 2 (IJ-slab sharding): as mode 0 and
  * dC[R*K] (dC holds R*K + 1 floats) receives this shard's ||S||^2 after the S-pass partials are

@@ -605,8 +605,24 @@ __device__ __forceinline__ AdamScalars adam_scalars_cached(const AdamCache& c, c
   return adam_scalars(ad, step);
 }
 
+// DEV: field by field as agent-scope write-through stores (read by other workgroups of a
+// persistent launch, qsc_scpass_loop)
+template <bool DEV = false>
 __device__ __forceinline__ void adam_cache_store(AdamCache* slots, const qsc_adam& ad, int step) {
-  slots[step & 1] = adam_cache_make(ad, step, adam_scalars(ad, step));
+  const AdamCache c = adam_cache_make(ad, step, adam_scalars(ad, step));
+  if constexpr (DEV) {
+    AdamCache* d = slots + (step & 1);
+    __hip_atomic_store(&d->tag, c.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&d->lr, c.lr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&d->b1, c.b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&d->b2, c.b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&d->eps, c.eps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&d->step_size, c.step_size, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&d->bc2_sqrt, c.bc2_sqrt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&d->rbc2, c.rbc2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    slots[step & 1] = c;
+  }
 }
 
 // One Adam element update (torch 2.x single-tensor path):
@@ -667,6 +683,22 @@ __device__ __forceinline__ float adam_row_fast(float (&p)[RH], float (&m)[RH], f
     f2v mm = f2v{m[j], m[j + 1]}, vv = f2v{v[j], v[j + 1]};
     mm = fma2(splat2(s.w1), g - mm, mm);
     vv = fma2(splat2(s.w2) * g, g, vv * splat2(s.beta2));
+#if QSC_ADAM_S_EST
+    // hardware sqrt / reciprocal estimates without the residual corrections (a few ulp from
+    // torch's correctly rounded sqrt and divisions; experimental, QSC_ADAM_S_EST=1 builds)
+    {
+      const f2v sq = f2v{__builtin_amdgcn_sqrtf(vv.x), __builtin_amdgcn_sqrtf(vv.y)};
+      const f2v den = fma2(sq, splat2(s.rbc2), splat2(s.eps));
+      const f2v pn = fma2(splat2(-s.step_size) * mm, rcp2(den), pp);
+      p[j] = (proj && pn.x < 0.0f) ? 0.0f : pn.x;
+      p[j + 1] = (proj && pn.y < 0.0f) ? 0.0f : pn.y;
+      m[j] = mm.x;
+      m[j + 1] = mm.y;
+      v[j] = vv.x;
+      v[j + 1] = vv.y;
+      continue;
+    }
+#endif
     // sqrt_fix
     const f2v sq = f2v{__builtin_amdgcn_sqrtf(vv.x), __builtin_amdgcn_sqrtf(vv.y)};
     const f2v er = fma2(-sq, sq, vv);

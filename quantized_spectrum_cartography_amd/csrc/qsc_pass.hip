@@ -1481,7 +1481,8 @@ struct FusedBlock {
 // One pixel tile t of nt of the fused launch (scfused_kernel, scfin_kernel: t = the workgroup).
 // C is read-only here; scfin_kernel's C-finish writes it after every tile has finished.
 template <int RP, typename E, int KIND, bool LOG, bool FIN = false>
-__device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const int nt) {
+__device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const int nt,
+                                             const unsigned tidx) {
   using V4 = typename Ent<E>::V4;
   constexpr int CP = TP<RP, KIND>::v;  // C^T row pitch == S tile row pitch
   constexpr int RH = RP / 2;
@@ -1497,7 +1498,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   const int U = nks * NP;
   float* Nl = Pl + (NP > 1 ? (size_t)U * R * 64 : 0);               // [max(U,16)]
   const int Kp = nks * 64;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tidx >> 6), lane = tidx & 63;
   const int p = lane & (QSC_SLICE - 1), h = lane >> 5;
   const float own_scale = own_scale_of<KIND, LOG>(lk);
   const int nsl = PT / QSC_SLICE;  // slices per tile
@@ -1513,7 +1514,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
 
   // 1. C^T / edge / state reads first (the LDS staging then waits only for them: vmcnt
   //    retires in issue order), then the first slice's reads, then the staging
-  const int k0 = threadIdx.x;
+  const int k0 = tidx;
 #if QSC_CT_VEC
   // C^T from 16-B reads of the [R][K] C: thread i holds C's flat floats 4i..4i+3 (one row r,
   // four consecutive bins) and writes them transposed; 32x fewer read instructions than a
@@ -1549,7 +1550,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   float nsq_s = 0.0f;
   int step_s = 0;
   AdamCache ac0{}, ac1{};
-  if (threadIdx.x == 0) {
+  if (tidx == 0) {
     nsq_s = st->normsq_s;
     step_s = st->step_s;
     ac0 = acache[0];  // both slots: no dependent read on step_s
@@ -1620,7 +1621,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     El[min(k0, nbins - 1)] = e0;
     for (int b = k0 + (int)blockDim.x; b < nbins; b += blockDim.x) El[b] = E_.e[b];
     STAMP(wg, 10);  // C^T rows written (its reads landed)
-    if (threadIdx.x == 0) {
+    if (tidx == 0) {
       const float nrm = sqrtf(nsq_s);
       sc.coef = nrm > 0.0f ? lambda_s / nrm : 0.0f;
       sc.as = adam_scalars_cached(((step_s + 1) & 1) ? ac1 : ac0, ad, step_s + 1);
@@ -1650,14 +1651,14 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     // chain of dependent global reads at the end it delayed the last workgroup); the order of
     // cnorm_sq: thread t < 256 accumulates flat indices t, t + 256, ..., then block_sum
     float s2 = 0.0f;
-    if (threadIdx.x < 256)
-      for (int i = threadIdx.x; i < R * K; i += 256) {
+    if (tidx < 256)
+      for (int i = tidx; i < R * K; i += 256) {
         const int r = i / K, k = i - r * K;
         const float c = Cl[k * CP + r];
         s2 = __builtin_fmaf(c, c, s2);
       }
     const float nsq = block_sum(s2, Nl);
-    if (threadIdx.x == 0) st_fin<FIN>(cnsq, nsq);
+    if (tidx == 0) st_fin<FIN>(cnsq, nsq);
   }
 
   // 2. S-step over the wave's slices (next slice's reads in flight; the two register sets
@@ -1815,7 +1816,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
 
   // the next launch's S-step scalars, by the oldest wave of block 0 (it has slack: its slices
   // are done long before the tile barrier)
-  if (t == 0 && threadIdx.x == 0) adam_cache_store(acache, ad, step_s + 2);
+  if (t == 0 && tidx == 0) adam_cache_store<FIN>(acache, ad, step_s + 2);
 
   STAMP(wg, 2);
   if (u < U) {
@@ -1845,7 +1846,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   STAMP(wg, 4);
   if (NP > 1) {
     __syncthreads();
-    for (int i = threadIdx.x, j = 0; i < nks * R * 64; i += blockDim.x, ++j) {
+    for (int i = tidx, j = 0; i < nks * R * 64; i += blockDim.x, ++j) {
       const int ks = i / (R * 64), rl = i - ks * (R * 64);
       const float* pp0 = Pl + (size_t)ks * NP * R * 64 + rl;
       float acc = pp0[0];
@@ -1858,7 +1859,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
 #endif
       st_fin<FIN>(&slab[((int64_t)t * R + r) * Kp + kk], acc);
     }
-    for (int ks = threadIdx.x; ks < nks; ks += blockDim.x) {
+    for (int ks = tidx; ks < nks; ks += blockDim.x) {
       float acc = Nl[ks * NP];
       for (int pp = 1; pp < NP; ++pp) acc += Nl[ks * NP + pp];
       st_fin<FIN>(&part_nll_c[t * nks + ks], acc);
@@ -1870,7 +1871,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
 
 template <int RP, typename E, int KIND, bool LOG>
 __global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(QSC_SCF_KPARAMS) {
-  scfused_tile<RP, E, KIND, LOG>(QSC_SCF_ARGS, (int)blockIdx.x, (int)gridDim.x);
+  scfused_tile<RP, E, KIND, LOG>(QSC_SCF_ARGS, (int)blockIdx.x, (int)gridDim.x, threadIdx.x);
 }
 
 // LDS bytes of scfused_kernel
@@ -1930,6 +1931,7 @@ constexpr int kFWaves = kFBlock / 64;
 
 // C-finish work item vb of R*nks + 2 (cfinish_kernel: vb = the workgroup; scfin_kernel: one
 // item per late-arriving workgroup), with its LDS scratch passed in
+template <bool DEV = false>
 __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scalars& sc,
                                            float (*sh3)[kFWaves], QSC_CF_PARAMS) {
   constexpr int NW = kFWaves;
@@ -1942,7 +1944,7 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
 
   if (vb == R * nks + 1) {
     // the next C-step's Adam scalars (the next S-pass settles step_c + 1 in between)
-    if (mode == 1 && threadIdx.x == 0) adam_cache_store(acache, ad, st->step_c + 2);
+    if (mode == 1 && threadIdx.x == 0) adam_cache_store<DEV>(acache, ad, st->step_c + 2);
     return;
   }
   if (vb == R * nks) {
@@ -1987,9 +1989,10 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
         sq += sh3[1][w];
         tot += sh3[2][w];
       }
+      int pnd = pend;
       if (settle) {  // settle_s, thread-0 part
         const int it = st->iter - 1;
-        st->nll_s = sn;
+        st_fin<DEV>(&st->nll_s, sn);
         if (hist && it >= 0 && it < hist_cap) {
           hist[4 * it + 0] = st->nll_c;
           hist[4 * it + 1] = sn;
@@ -1997,15 +2000,16 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
           hist[4 * it + 3] = st->normsq_s_prev;
         }
         if (supd) {
-          st->normsq_s = sq;
-          st->step_s += 1;
+          st_fin<DEV>(&st->normsq_s, sq);
+          st_fin<DEV>(&st->step_s, st->step_s + 1);
         }
-        st->pending = pend & ~(QSC_PEND_SNLL | QSC_PEND_SUPD);
+        pnd = pend & ~(QSC_PEND_SNLL | QSC_PEND_SUPD);
+        st_fin<DEV>(&st->pending, pnd);
       }
-      st->nll_c = tot;
+      st_fin<DEV>(&st->nll_c, tot);
       if (mode == 1) {
-        st->normsq_c = nsq;
-        st->pending |= QSC_PEND_C;
+        st_fin<DEV>(&st->normsq_c, nsq);
+        st_fin<DEV>(&st->pending, pnd | QSC_PEND_C);
       }
       if (mode == 2) dC[(int64_t)R * K] = st->normsq_s;  // this shard's ||S||^2 (IJ-slab)
     }
@@ -2055,9 +2059,9 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
       float p = p0, m = m0, v = v0;
       g = __fadd_rn(g, __fmul_rn(p, sc.coef));
       adam_elem(p, m, v, g, ad, sc.as);
-      C[i] = p;
-      mC[i] = m;
-      vC[i] = v;
+      st_fin<DEV>(&C[i], p);
+      st_fin<DEV>(&mC[i], m);
+      st_fin<DEV>(&vC[i], v);
     } else {
       dC[i] = g;  // modes 0 and 2
     }
@@ -2093,7 +2097,8 @@ template <int RP, typename E, int KIND, bool LOG>
 __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
     QSC_SCFIN_KPARAMS, float* __restrict__ mC, float* __restrict__ vC, qsc_adam adc,
     float lambda_c, float* __restrict__ hist, int hist_cap, AdamCache* __restrict__ acache_c) {
-  scfused_tile<RP, E, KIND, LOG, true>(QSC_SCF_ARGS, (int)blockIdx.x, (int)gridDim.x);
+  scfused_tile<RP, E, KIND, LOG, true>(QSC_SCF_ARGS, (int)blockIdx.x, (int)gridDim.x,
+                                       threadIdx.x);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int nt = gridDim.x, nvb = R * nks + 2;
   // C-finish scratch and the arrival broadcast word, over the (now idle) tile LDS
@@ -2150,6 +2155,175 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
              nt * PT / QSC_SLICE, hist, hist_cap, acache_c);
   STAMP(wg, 21);  // C-finish item done
 }
+
+// ---------------------------------------------------------------------------------------
+// Persistent fused loop (qsc_scpass_loop): n fused bodies (S-step i + C-pass i+1 + that
+// C-step's finish) in ONE launch.  One workgroup per tile for the whole launch (every
+// workgroup co-resident: the host checks occupancy x CUs >= tiles).  Per iteration: the tile
+// body and the fused-finish tail of scfin_kernel, every cross-workgroup value stored write-
+// through at agent scope (st_fin, cfinish_vb<true>); each finishing workgroup then counts its
+// item in the state's fin_done word, and every workgroup waits for the iteration's R*nks + 2
+// items before the next tile body (one acquire fence: C, the state and the Adam cache were
+// written by other workgroups).  What a kernel boundary costs per iteration -- the drain, the
+// dispatch of 256 workgroups, kernel-argument reads, the cold start of every wave -- is gone;
+// S, mS and vS rows stay in the XCD's L2 between iterations (each tile reads back only its own
+// rows, written by the same wave).  The arguments are read every iteration from the kernarg segment
+// through an offset laundered by an empty asm, and so are the workgroup and thread indices:
+// nothing derived from them is hoisted out of the loop and kept live across it (a first
+// persistent attempt spilled 113 SGPRs keeping the arguments; as plain kernel arguments inside
+// a loop they are not rematerialised as in the one-shot kernels: 202 SGPR spills).  A wait past kFinSpin
+// polls sets fused_fault and every workgroup leaves the loop.
+struct LoopArgs {
+  const void* s_ent;
+  const int* s_width;
+  const int64_t* s_off;
+  const void* c_ent;
+  const int* c_width;
+  const int64_t* c_off;
+  const int* c_kmap;
+  float* S;
+  float* C;
+  float* mS;
+  float* vS;
+  qsc_state* st;
+  float* part_nll_s;
+  float* part_nsq_s;
+  float* slab;
+  float* part_nll_c;
+  float* cnsq;
+  AdamCache* acache;
+  float* mC;
+  float* vC;
+  float* hist;
+  AdamCache* acache_c;
+  qsc_adam ad;
+  qsc_adam adc;
+  Lik lk;
+  float lambda_s, lambda_c;
+  int nks, NP, PT, nbins, R, K, hist_cap, n;
+  int* progress;  // nullable diagnostics: per workgroup, 16 * iteration + phase reached
+  Edges E;
+};
+using LoopKA = const char __attribute__((address_space(4)));
+#define QSC_LA(f) (*(const decltype(LoopArgs::f)*)(const char*)(kb + offsetof(LoopArgs, f)))
+
+// one iteration of scloop_kernel (kb, t and tidx laundered by the caller); false: leave the loop
+template <int RP, typename E, int KIND, bool LOG>
+__device__ __forceinline__ bool scloop_iter(LoopKA* kb, const int t, const unsigned tidx, int it,
+                                            int n, unsigned long long done0) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int nt = (int)gridDim.x;
+  qsc_state* st = QSC_LA(st);
+  const int R = QSC_LA(R), nks = QSC_LA(nks);
+  const Edges& E_ = *(const Edges*)(const char*)(kb + offsetof(LoopArgs, E));
+  int* const prog = QSC_LA(progress);
+  auto mark = [&](int phase) {
+    if (prog && tidx == 0)
+      __hip_atomic_store(prog + t, 16 * it + phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  mark(1);
+  scfused_tile<RP, E, KIND, LOG, true>(
+      reinterpret_cast<const E*>(QSC_LA(s_ent)), QSC_LA(s_width), QSC_LA(s_off),
+      reinterpret_cast<const E*>(QSC_LA(c_ent)), QSC_LA(c_width), QSC_LA(c_off), QSC_LA(c_kmap),
+      nks, QSC_LA(NP), QSC_LA(PT), QSC_LA(lk), E_, QSC_LA(nbins), R, QSC_LA(K), QSC_LA(S),
+      QSC_LA(C), QSC_LA(mS), QSC_LA(vS), QSC_LA(ad), QSC_LA(lambda_s), st, QSC_LA(part_nll_s),
+      QSC_LA(part_nsq_s), QSC_LA(slab), QSC_LA(part_nll_c), QSC_LA(cnsq), QSC_LA(acache),
+      nullptr, t, nt, tidx);
+  const int nvb = R * nks + 2;
+  float(*red)[64] = reinterpret_cast<float(*)[64]>(smem);
+  float(*sh3)[kFWaves] = reinterpret_cast<float(*)[kFWaves]>(smem + kFWaves * 64);
+  Scalars& sc = *reinterpret_cast<Scalars*>(smem + kFWaves * 64 + 3 * kFWaves);
+  int* vbl = reinterpret_cast<int*>(smem + kFWaves * 64 + 3 * kFWaves + 16);
+  unsigned long long* ticket = reinterpret_cast<unsigned long long*>(st) + 5;
+  unsigned long long* done = reinterpret_cast<unsigned long long*>(st) + 6;
+  int* fault = reinterpret_cast<int*>(st) + 9;
+  mark(2);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (st_fin stores complete: see scfin)
+  __syncthreads();
+  if (tidx == 0) {
+    const unsigned long long tk =
+        __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long a = tk % (unsigned long long)nt;
+    int vb = (int)a - (nt - nvb);
+    if (vb >= 0) {
+      const unsigned long long target = tk - a + (unsigned long long)nt;
+      unsigned polls = 0;
+      while (__hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        if (++polls > kFinSpin) {
+          __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          vb = -2;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (vb >= 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    *vbl = vb;
+  }
+  __syncthreads();
+  const int vb = *vbl;
+  mark(vb == -2 ? 9 : 3);
+  if (vb == -2) return false;  // (timed out: leave; the others time out on fin_done)
+  if (vb >= 0) {
+    cfinish_vb<true>(vb, red, sc, sh3, QSC_LA(slab), nt, nks, R, QSC_LA(K), QSC_LA(C), 1,
+                     nullptr, QSC_LA(mC), QSC_LA(vC), QSC_LA(adc), QSC_LA(lambda_c), nullptr,
+                     QSC_LA(cnsq), st, QSC_LA(part_nll_c), nt * nks, QSC_LA(part_nll_s),
+                     QSC_LA(part_nsq_s), nt * QSC_LA(PT) / QSC_SLICE, QSC_LA(hist),
+                     QSC_LA(hist_cap), QSC_LA(acache_c));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tidx == 0)
+      __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mark(4);
+  }
+  if (it + 1 >= n) return true;
+  // the next tile body reads C, the state and the Adam caches: wait for every C-finish item of
+  // this iteration, then one acquire fence
+  if (tidx == 0) {
+    const unsigned long long target = done0 + (unsigned long long)nvb * (unsigned long long)(it + 1);
+    unsigned polls = 0;
+    int ok = 1;
+    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++polls > kFinSpin) {
+        __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *vbl = ok;
+  }
+  __syncthreads();
+  const int ok = *vbl;
+  __syncthreads();  // (the LDS word is tile LDS again in the next body)
+  mark(ok ? 5 : 10);
+  return ok != 0;
+}
+
+template <int RP, typename E, int KIND, bool LOG>
+__global__ void __launch_bounds__(FusedBlock<RP>::v) scloop_kernel(LoopArgs args) {
+  LoopKA* const kp = (LoopKA*)__builtin_amdgcn_kernarg_segment_ptr();
+  int n = 0;
+  unsigned long long done0 = 0;
+  {
+    LoopKA* const kb = kp;
+    n = QSC_LA(n);
+    // the fin_done base: every finish of this launch completes after every workgroup has taken
+    // its first ticket, i.e. after this read (thread 0 keeps it)
+    if (threadIdx.x == 0)
+      done0 = __hip_atomic_load(reinterpret_cast<unsigned long long*>(QSC_LA(st)) + 6,
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  (void)args;
+  for (int it = 0; it < n; ++it) {
+    int o = 0, t = (int)blockIdx.x;
+    unsigned tidx = threadIdx.x;
+    asm volatile("" : "+s"(o), "+s"(t), "+v"(tidx));  // re-derived every iteration
+    if (!scloop_iter<RP, E, KIND, LOG>(kp + o, t, tidx, it, n, done0)) return;
+  }
+}
+#undef QSC_LA
 
 // ---------------------------------------------------------------------------------------
 // C update from an externally reduced gradient g [R][K] (IJ-slab sharding, after the RCCL
@@ -2845,6 +3019,119 @@ QSC_API int qsc_scpass_fin(const qsc_obs_desc* d, const void* s_entries, const i
   } while (0)
   QSC_DISPATCH_PASS(SCFIN_LAUNCH);
 #undef SCFIN_LAUNCH
+  QSC_CHECK_LAUNCH();
+  return QSC_OK;
+}
+
+// every workgroup of the persistent loop resident at once: tiles <= blocks per CU x CUs
+static bool loop_fits(const void* kp, unsigned threads, size_t shm, int ntiles) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kp, (int)threads, shm) != hipSuccess)
+    return false;
+  return ntiles <= nb * cu_count();
+}
+
+QSC_API int qsc_scpass_loop_supported(const qsc_obs_desc* d, int32_t R) {
+  if (!qsc_scpass_fin_supported(d, R)) return 0;
+  return d->ntiles <= cu_count() ? 1 : 0;  // one 16-wave workgroup per CU
+}
+
+QSC_API int qsc_scpass_loop(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
+                            const int64_t* s_off, const void* c_entries, const int32_t* c_width,
+                            const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
+                            int32_t R, float* S, float* C, float* mS, float* vS,
+                            const qsc_adam* adam_s, float lambda_s, float* mC, float* vC,
+                            const qsc_adam* adam_c, float lambda_c, qsc_state* st, float* hist,
+                            int32_t hist_cap, int32_t n_iter, void* ws, size_t ws_bytes,
+                            void* stream) {
+  return qsc_scpass_loop_dbg(d, s_entries, s_width, s_off, c_entries, c_width, c_off, c_kmap, m,
+                             R, S, C, mS, vS, adam_s, lambda_s, mC, vC, adam_c, lambda_c, st,
+                             hist, hist_cap, n_iter, nullptr, ws, ws_bytes, stream);
+}
+
+QSC_API int qsc_scpass_loop_dbg(const qsc_obs_desc* d, const void* s_entries,
+                                const int32_t* s_width, const int64_t* s_off,
+                                const void* c_entries, const int32_t* c_width,
+                                const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
+                                int32_t R, float* S, float* C, float* mS, float* vS,
+                                const qsc_adam* adam_s, float lambda_s, float* mC, float* vC,
+                                const qsc_adam* adam_c, float lambda_c, qsc_state* st,
+                                float* hist, int32_t hist_cap, int32_t n_iter, int32_t* progress,
+                                void* ws, size_t ws_bytes, void* stream) {
+  if (!qsc_scpass_loop_supported(d, R) || !m || m->nbounds - 1 != d->nbins || !S || !C || !mS ||
+      !vS || !adam_s || !mC || !vC || !adam_c || !st || !s_width || !s_off || !c_width ||
+      !c_off || !c_kmap || (d->s_entries > 0 && !s_entries) ||
+      (d->c_entries > 0 && !c_entries) || !ws || ws_bytes < ws_bytes_for(d, R) ||
+      (hist_cap > 0 && !hist) || n_iter < 0)
+    return QSC_EINVAL;
+  if (n_iter == 0) return QSC_OK;
+  const int kind = lik_kind(m);
+  const bool sr = d->rowfmt == 1;
+  if (!rowfmt_ok(d, R, kind)) return QSC_EINVAL;
+  const int RP = rp_of(R);
+  const int NP = cpass_parts(d, R, sr);
+  const size_t shm = scfused_lds(d->PT, R, d->K, d->nks, NP, sr);
+  PassWs w = carve(d, R, ws);
+  LoopArgs la{};
+  make_edges(m, &la.E);
+  la.lk = make_lik(m);
+  set_dbg(la.lk, d, sr);
+  if (kind == LIK_SQUARED)
+    make_sq_targets(m, &la.E);
+  else if (!m->log_model)
+    scale_edges(&la.E, m->nbounds - 1, la.lk.a);
+  la.s_ent = s_entries;
+  la.s_width = s_width;
+  la.s_off = s_off;
+  la.c_ent = c_entries;
+  la.c_width = c_width;
+  la.c_off = c_off;
+  la.c_kmap = c_kmap;
+  la.S = S;
+  la.C = C;
+  la.mS = mS;
+  la.vS = vS;
+  la.st = st;
+  la.part_nll_s = w.snll;
+  la.part_nsq_s = w.snsq;
+  la.slab = w.slab;
+  la.part_nll_c = w.cnll;
+  la.cnsq = w.cnsq;
+  la.acache = w.acache;
+  la.mC = mC;
+  la.vC = vC;
+  la.hist = hist;
+  la.acache_c = w.acache + 2;
+  la.ad = *adam_s;
+  la.adc = *adam_c;
+  la.lambda_s = lambda_s;
+  la.lambda_c = lambda_c;
+  la.nks = d->nks;
+  la.NP = NP;
+  la.PT = d->PT;
+  la.nbins = d->nbins;
+  la.R = R;
+  la.K = d->K;
+  la.hist_cap = hist_cap;
+  la.n = n_iter;
+  la.progress = progress;
+  const unsigned threads = scpass_threads(d, R);
+  (void)RP;
+  hipStream_t s = STREAM(stream);
+#define SCLOOP_LAUNCH(RPV, ET, KD, LG)                                                         \
+  do {                                                                                         \
+    if constexpr (RPV <= 8) {                                                                  \
+      if (!loop_fits(reinterpret_cast<const void*>(scloop_kernel<RPV, ET, KD, LG>), threads,   \
+                     shm, d->ntiles))                                                          \
+        return QSC_EUNSUPPORTED;                                                               \
+      hipLaunchKernelGGL((scloop_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles),          \
+                         dim3(threads), shm, s, la);                                           \
+    } else {                                                                                   \
+      return QSC_EUNSUPPORTED;                                                                 \
+    }                                                                                          \
+  } while (0)
+  QSC_DISPATCH_PASS(SCLOOP_LAUNCH);
+#undef SCLOOP_LAUNCH
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }

@@ -121,6 +121,24 @@ class PassEngine:
                   _lib.ptr(vC), adam_c, float(lambda_c), _lib.ptr(self.state), _lib.ptr(hist),
                   cap, _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
 
+    def scpass_loop_supported(self):
+        return bool(_lib.lib().qsc_scpass_loop_supported(self.desc, self.R))
+
+    def scpass_loop(self, S_pos, C, mS, vS, adam_s, lambda_s, mC, vC, adam_c, lambda_c, n,
+                    record=True, progress=None):
+        """n fused bodies (scpass_fin, bit for bit) in ONE persistent launch (qsc_scpass_loop):
+        one workgroup per tile for the whole launch, a device-wide wait for the C-finish
+        between bodies."""
+        o = self.obs
+        hist, cap = (self.hist, self.hist_cap) if (record and self.hist_cap) else (None, 0)
+        _lib.call("qsc_scpass_loop_dbg", self.desc, _lib.ptr(self.s_entries),
+                  _lib.ptr(o.s_width), _lib.ptr(o.s_off), _lib.ptr(self.c_entries),
+                  _lib.ptr(o.c_width), _lib.ptr(o.c_off), _lib.ptr(o.c_kmap), o.model, self.R,
+                  _lib.ptr(S_pos), _lib.ptr(C), _lib.ptr(mS), _lib.ptr(vS), adam_s,
+                  float(lambda_s), _lib.ptr(mC), _lib.ptr(vC), adam_c, float(lambda_c),
+                  _lib.ptr(self.state), _lib.ptr(hist), cap, int(n), _lib.ptr(progress),
+                  _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
+
     def supdate(self, S_pos, mS, vS, g, adam, lambda_s):
         _lib.call("qsc_supdate", self.desc, self.R, _lib.ptr(S_pos), _lib.ptr(mS), _lib.ptr(vS),
                   _lib.ptr(g), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),

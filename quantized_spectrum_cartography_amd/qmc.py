@@ -52,8 +52,11 @@ def issue_iterations(solver, n):
     finish): c_step, fused_body x (n-1), s_step -- two launches per iteration."""
     if getattr(solver, "fuse", False) and n >= 2:
         solver.c_step()
-        for _ in range(n - 1):
-            solver.fused_body()
+        if getattr(solver, "loop", False):
+            solver.fused_loop(n - 1)  # the n - 1 fused bodies in one persistent launch
+        else:
+            for _ in range(n - 1):
+                solver.fused_body()
         solver.s_step()
     else:
         for _ in range(n):
@@ -224,7 +227,7 @@ class FreeSSolver:
 
     def __init__(self, obs, S_init, C_init, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
                  betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024, fuse=True,
-                 T_true=None, nmse_every=0, fin=None, project_s=False):
+                 T_true=None, nmse_every=0, fin=None, project_s=False, loop=None):
         self.obs = obs
         R = S_init.shape[0]
         self.R = R
@@ -262,6 +265,15 @@ class FreeSSolver:
             fin = os.environ.get("QSC_FIN", "0") == "1"
         self.fin = (self.fuse and bool(fin) and not self.nmse_every
                     and self.engine.scpass_fin_supported())
+        # the fused bodies of a run in ONE persistent launch (qsc_scpass_loop: every tile's
+        # workgroup resident, a device-wide wait for the C-finish between bodies); opt-in with
+        # loop=True / QSC_LOOP=1 where supported, implies the fused finish
+        if loop is None:
+            loop = os.environ.get("QSC_LOOP", "0") == "1"
+        self.loop = (self.fuse and bool(loop) and not self.nmse_every
+                     and self.engine.scpass_loop_supported())
+        if self.loop:
+            self.fin = True
 
     # one outer iteration = C grad-step + S grad-step
     def c_step(self):
@@ -289,6 +301,11 @@ class FreeSSolver:
         e.scpass(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s)
         self._track()  # (S_{i+1}, C_{i+1}): C is updated by the cfinish below
         e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)
+
+    def fused_loop(self, n):
+        """n fused bodies (fused_body with `fin`, bit for bit) in one persistent launch."""
+        self.engine.scpass_loop(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s,
+                                self.mC, self.vC, self.adam_c, self.lambda_c, n)
 
     def _track(self):
         if not self.nmse_every:
