@@ -106,9 +106,9 @@ typedef struct qsc_state {
   float normsq_s_prev; /* ||S||^2 the last S-pass was evaluated with */
   int32_t fused_fault; /* sticky: 1 after a qsc_scpass_fin launch whose C-finish wait timed
                           out (the launch's C update is then incomplete: results invalid) */
-  uint64_t fin_ticket; /* qsc_scpass_fin arrival counter, never wraps (zeroed by qsc_state_init) */
-  uint64_t fin_done;   /* qsc_scpass_loop: C-finish work items completed, never wraps (zeroed) */
-  float reserved[2];
+  uint64_t fin_ticket; /* retired (round 3's fused-finish ticket; the arrival counters now live
+                          on lines of their own in the pass workspace, qsc_pass_sync_offset) */
+  float reserved[4];
 } qsc_state;
 
 /* Packed observation layout, produced by qsc_obs_layout (host struct).
@@ -460,6 +460,10 @@ QSC_API int qsc_cpass_nsq(const qsc_obs_desc* d, const void* c_entries, const in
 /* byte offset, in the pass workspace, of the float where qsc_cpass / qsc_cpass_nsq leave ||C||^2
  * of the C they read (the fixed order of qsc_sumsq_small): a K-slab solver all-reduces it in
  * place and hands it to qsc_cfinish as normsq_c_ext.  -1 on an invalid descriptor. */
+/* byte offset in the pass workspace of the fused-finish launches' counters (two uint64 on
+ * 128-B lines of their own: arrival tickets, then the persistent loop's completed C-finish
+ * items), for diagnostics; the workspace must be zero-filled before its first use */
+QSC_API int64_t qsc_pass_sync_offset(const qsc_obs_desc* d, int32_t R);
 QSC_API int64_t qsc_pass_cnsq_offset(const qsc_obs_desc* d, int32_t R);
 /* ||x||^2 into *out (fp32, fixed order), e.g. the local ||C_slab||^2 before an all-reduce */
 QSC_API int qsc_sumsq_small(const float* x, int32_t n, float* out, void* stream);

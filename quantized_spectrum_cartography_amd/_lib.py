@@ -205,13 +205,6 @@ def read_state(st):
     return out
 
 
-def read_counters(st):
-    """(fin_ticket, fin_done) of a device qsc_state: the fused-finish arrival count and the
-    persistent loop's completed C-finish items (synchronises; diagnostics)."""
-    raw = st.detach().cpu()
-    return int(raw[40:48].view(torch.int64).item()), int(raw[48:56].view(torch.int64).item())
-
-
 def state_field(st, name):
     """A 1-element device view of one float field of a qsc_state tensor."""
     o = STATE_OFFSETS[name]

@@ -855,6 +855,36 @@ __device__ __forceinline__ void st_row(float* __restrict__ base, uint32_t lo, co
   }
 }
 
+// The same store written through this XCD's L2 (agent-scope sc1 buffer stores): the line is not
+// left dirty in L2, so the end-of-launch write-back has less to drain (the S-step's S, mS, vS
+// rows are 25 MB per launch at C3; MI355X_MICROARCH.md prices a boundary at +B / 6 TB/s for B
+// dirty bytes).  Byte offsets from `base` below 2^31.
+#ifndef QSC_WT_S
+#define QSC_WT_S 0
+#endif
+template <int N>
+__device__ __forceinline__ void st_row_wt(float* base, uint32_t lo, const float (&v)[N]) {
+#if QSC_WT_S
+  typedef unsigned u4v __attribute__((ext_vector_type(4)));
+  typedef unsigned u2v __attribute__((ext_vector_type(2)));
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff,
+                                                                     0x00020000);
+  if constexpr (N == 2) {
+    const u2v w = {__float_as_uint(v[0]), __float_as_uint(v[1])};
+    __builtin_amdgcn_raw_buffer_store_b64(w, r, lo, 0, 16);  // aux 16: sc1
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; i += 4) {
+      const u4v w = {__float_as_uint(v[i]), __float_as_uint(v[i + 1]), __float_as_uint(v[i + 2]),
+                     __float_as_uint(v[i + 3])};
+      __builtin_amdgcn_raw_buffer_store_b128(w, r, lo + 16 * (i / 4), 0, 16);
+    }
+  }
+#else
+  st_row<N>(base, lo, v);
+#endif
+}
+
 // Per-slice registers read from HBM: the first group of entry chunks, S[:, q] and (fused Adam)
 // the moments of the lane's rows.  Two sets live at once (current + prefetched next slice).
 template <int RP, typename E, bool ADAM>
@@ -1707,9 +1737,9 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     }
     float nsq = adam_row_fast<RH>(pv, m, v, a, sc.coef, sc.as, ad.project_nonneg != 0);
     const int64_t blk = (int64_t)s * QSC_SLICE * RP;  // the slice's rows (uniform)
-    st_row<RH>(S + blk, ln.half, pv);
-    st_row<RH>(mS + blk, ln.half, m);
-    st_row<RH>(vS + blk, ln.half, v);
+    st_row_wt<RH>(S + blk, ln.half, pv);
+    st_row_wt<RH>(mS + blk, ln.half, m);
+    st_row_wt<RH>(vS + blk, ln.half, v);
     st_row<RH>(Sl + (il * QSC_SLICE + p) * CP + h * RH, pv);  // the tile row, for the C-pass
     if constexpr (is_sr(KIND)) {
       float nv[RH];
@@ -2096,7 +2126,8 @@ constexpr unsigned kFinSpin = 1u << 20;
 template <int RP, typename E, int KIND, bool LOG>
 __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
     QSC_SCFIN_KPARAMS, float* __restrict__ mC, float* __restrict__ vC, qsc_adam adc,
-    float lambda_c, float* __restrict__ hist, int hist_cap, AdamCache* __restrict__ acache_c) {
+    float lambda_c, float* __restrict__ hist, int hist_cap, AdamCache* __restrict__ acache_c,
+    unsigned long long* sync) {
   scfused_tile<RP, E, KIND, LOG, true>(QSC_SCF_ARGS, (int)blockIdx.x, (int)gridDim.x,
                                        threadIdx.x);
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -2106,9 +2137,9 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
   float(*sh3)[kFWaves] = reinterpret_cast<float(*)[kFWaves]>(smem + kFWaves * 64);
   Scalars& sc = *reinterpret_cast<Scalars*>(smem + kFWaves * 64 + 3 * kFWaves);
   int* vbl = reinterpret_cast<int*>(smem + kFWaves * 64 + 3 * kFWaves + 16);
-  // qsc_state.fin_ticket (64-bit: it counts every workgroup of every launch for the life of
-  // the state, and must stay aligned to launches, so it may never wrap)
-  unsigned long long* ticket = reinterpret_cast<unsigned long long*>(st) + 5;
+  // the arrival ticket (PassWs::sync[0]; 64-bit: it counts every workgroup of every launch for
+  // the life of the workspace, and must stay aligned to launches, so it may never wrap)
+  unsigned long long* ticket = sync;
   int* fault = reinterpret_cast<int*>(st) + 9;              // qsc_state.fused_fault
   // Ordering, chosen for the 8 non-coherent XCD L2s: everything the C-finish items read was
   // stored write-through at agent scope by the tile body (st_fin), so each wave waits for its
@@ -2202,6 +2233,7 @@ struct LoopArgs {
   float lambda_s, lambda_c;
   int nks, NP, PT, nbins, R, K, hist_cap, n;
   int* progress;  // nullable diagnostics: per workgroup, 16 * iteration + phase reached
+  unsigned long long* sync;  // PassWs::sync: [0] tickets, [16] completed C-finish items
   Edges E;
 };
 using LoopKA = const char __attribute__((address_space(4)));
@@ -2234,8 +2266,9 @@ __device__ __forceinline__ bool scloop_iter(LoopKA* kb, const int t, const unsig
   float(*sh3)[kFWaves] = reinterpret_cast<float(*)[kFWaves]>(smem + kFWaves * 64);
   Scalars& sc = *reinterpret_cast<Scalars*>(smem + kFWaves * 64 + 3 * kFWaves);
   int* vbl = reinterpret_cast<int*>(smem + kFWaves * 64 + 3 * kFWaves + 16);
-  unsigned long long* ticket = reinterpret_cast<unsigned long long*>(st) + 5;
-  unsigned long long* done = reinterpret_cast<unsigned long long*>(st) + 6;
+  unsigned long long* const sync = QSC_LA(sync);
+  unsigned long long* ticket = sync;
+  unsigned long long* done = sync + 16;
   int* fault = reinterpret_cast<int*>(st) + 9;
   mark(2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (st_fin stores complete: see scfin)
@@ -2312,8 +2345,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scloop_kernel(LoopArgs args
     // the fin_done base: every finish of this launch completes after every workgroup has taken
     // its first ticket, i.e. after this read (thread 0 keeps it)
     if (threadIdx.x == 0)
-      done0 = __hip_atomic_load(reinterpret_cast<unsigned long long*>(QSC_LA(st)) + 6,
-                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      done0 = __hip_atomic_load(QSC_LA(sync) + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   (void)args;
   for (int it = 0; it < n; ++it) {
@@ -2513,6 +2545,13 @@ struct PassWs {
   int* sched;       // S-pass queue counters [kSchedQ] + finished-wave counter (zero between launches)
   float* cnsq;      // ||C||^2 of the C the last C-pass read (written by the C-pass)
   AdamCache* acache;  // [0..1] S-side, [2..3] C-side step scalars (adam_scalars_cached)
+  // cross-workgroup counters of the fused-finish launches, each on a 128-B line of its own that
+  // only atomics and agent-scope (sc1) loads touch: [0] arrival tickets, [16] the persistent
+  // loop's completed C-finish items.  An sc1 load is served by the XCD's L2, so a counter on a
+  // line that plain loads also bring into an L2 (the state's other fields) can be read stale
+  // there for as long as the line stays (seen: a persistent-loop wait that never ended).
+  // Zero-filled with the workspace; they only ever count up.
+  unsigned long long* sync;
 };
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -2536,6 +2575,8 @@ PassWs carve(const qsc_obs_desc* d, int R, void* ws) {
   p.cnsq = (float*)w;
   w += al(4);
   p.acache = (AdamCache*)w;
+  w += al(4 * sizeof(AdamCache));
+  p.sync = (unsigned long long*)w;
   return p;
 }
 
@@ -2543,7 +2584,7 @@ size_t ws_bytes_for(const qsc_obs_desc* d, int R) {
   const int64_t Kp = (int64_t)d->nks * 64;
   return al((size_t)d->ntiles * R * Kp * 4) + al((size_t)d->ntiles * d->nks * 4) +
          2 * al((size_t)(d->Pp / QSC_SLICE) * 4) + al(256 * 8) + al((kSchedQ + 1) * 4) + al(4) +
-         al(4 * sizeof(AdamCache));
+         al(4 * sizeof(AdamCache)) + al(32 * sizeof(unsigned long long));
 }
 
 bool desc_ok(const qsc_obs_desc* d) {
@@ -2735,6 +2776,13 @@ QSC_API int qsc_cpass_nsq(const qsc_obs_desc* d, const void* c_entries, const in
                           void* stream) {
   return cpass_impl(d, c_entries, c_width, c_off, c_kmap, m, R, S, C, ws, ws_bytes, stream,
                     true);
+}
+
+QSC_API int64_t qsc_pass_sync_offset(const qsc_obs_desc* d, int32_t R) {
+  if (!desc_ok(d) || R < 1 || R > QSC_MAX_R) return -1;
+  const uintptr_t base = 4096;
+  return (int64_t)(reinterpret_cast<uintptr_t>(carve(d, R, reinterpret_cast<void*>(base)).sync) -
+                   base);
 }
 
 QSC_API int64_t qsc_pass_cnsq_offset(const qsc_obs_desc* d, int32_t R) {
@@ -3012,7 +3060,7 @@ QSC_API int qsc_scpass_fin(const qsc_obs_desc* d, const void* s_entries, const i
                          (const ET*)c_entries, c_width, c_off, c_kmap, d->nks, NP, d->PT, lk,  \
                          E, d->nbins, R, d->K, S, C, mS, vS, ad, lambda_s, st, w.snll, w.snsq, \
                          w.slab, w.cnll, w.cnsq, w.acache, (const int*)nullptr, mC, vC,        \
-                         adc, lambda_c, hist, hist_cap, w.acache + 2);                         \
+                         adc, lambda_c, hist, hist_cap, w.acache + 2, w.sync);                 \
     } else {                                                                                   \
       return QSC_EUNSUPPORTED;                                                                 \
     }                                                                                          \
@@ -3115,6 +3163,7 @@ QSC_API int qsc_scpass_loop_dbg(const qsc_obs_desc* d, const void* s_entries,
   la.hist_cap = hist_cap;
   la.n = n_iter;
   la.progress = progress;
+  la.sync = w.sync;
   const unsigned threads = scpass_threads(d, R);
   (void)RP;
   hipStream_t s = STREAM(stream);

@@ -121,6 +121,15 @@ class PassEngine:
                   _lib.ptr(vC), adam_c, float(lambda_c), _lib.ptr(self.state), _lib.ptr(hist),
                   cap, _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
 
+    def fin_counters(self):
+        """(arrival tickets, completed C-finish items) of the fused-finish launches on this
+        engine's workspace (diagnostics; synchronises)."""
+        off = int(_lib.lib().qsc_pass_sync_offset(self.desc, self.R))
+        if off < 0:
+            raise _lib.QscError("qsc_pass_sync_offset failed")
+        raw = self.ws[off:off + 256].cpu()
+        return int(raw[0:8].view(torch.int64).item()), int(raw[128:136].view(torch.int64).item())
+
     def scpass_loop_supported(self):
         return bool(_lib.lib().qsc_scpass_loop_supported(self.desc, self.R))
 

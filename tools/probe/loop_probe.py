@@ -54,8 +54,7 @@ def main():
           flush=True)
     print("laggards", [(i, v) for i, v in enumerate(pv) if v != max(pv)][:20], flush=True)
     sb = b.state()
-    from quantized_spectrum_cartography_amd import _lib
-    tk, dn = _lib.read_counters(b.engine.state)
+    tk, dn = b.engine.fin_counters()
     nvb = R * o.desc.nks + 2
     print("fused_fault", sb["fused_fault"], "tickets", tk, "expected", (n - 1) * o.desc.ntiles,
           "finish items done", dn, "expected", (n - 1) * nvb, flush=True)
