@@ -860,7 +860,7 @@ __device__ __forceinline__ void st_row(float* __restrict__ base, uint32_t lo, co
 // rows are 25 MB per launch at C3; MI355X_MICROARCH.md prices a boundary at +B / 6 TB/s for B
 // dirty bytes).  Byte offsets from `base` below 2^31.
 #ifndef QSC_WT_S
-#define QSC_WT_S 0
+#define QSC_WT_S 1
 #endif
 template <int N>
 __device__ __forceinline__ void st_row_wt(float* base, uint32_t lo, const float (&v)[N]) {
@@ -1107,13 +1107,13 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
         v[j] = c.vv[j];
       }
       float nsq = adam_row_fast<RH>(pv, m, v, a, sc.coef, sc.as, ad.project_nonneg != 0);
-      st_row<RH>(S + blk, ln.half, pv);
-      st_row<RH>(mS + blk, ln.half, m);
-      st_row<RH>(vS + blk, ln.half, v);
+      st_row_wt<RH>(S + blk, ln.half, pv);
+      st_row_wt<RH>(mS + blk, ln.half, m);
+      st_row_wt<RH>(vS + blk, ln.half, v);
       nsq = wave_sum_dpp(nsq);
       if (lane == 0) part_nsq[s] = nsq;
     } else {
-      st_row<RH>(dS + blk, ln.half, a);
+      st_row_wt<RH>(dS + blk, ln.half, a);
     }
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (lane == 0) part_nll[s] = nll_w;
@@ -2204,6 +2204,8 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
 // persistent attempt spilled 113 SGPRs keeping the arguments; as plain kernel arguments inside
 // a loop they are not rematerialised as in the one-shot kernels: 202 SGPR spills).  A wait past kFinSpin
 // polls sets fused_fault and every workgroup leaves the loop.
+constexpr int kLoopTimeout = -0x40000000;  // the ticket wait timed out (vb sentinel)
+
 struct LoopArgs {
   const void* s_ent;
   const int* s_width;
@@ -2277,14 +2279,15 @@ __device__ __forceinline__ bool scloop_iter(LoopKA* kb, const int t, const unsig
     const unsigned long long tk =
         __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long a = tk % (unsigned long long)nt;
-    int vb = (int)a - (nt - nvb);
+    int vb = (int)a - (nt - nvb);  // >= 0: a C-finish item; -1: none; kLoopTimeout: timed out
+    if (vb < 0) vb = -1;
     if (vb >= 0) {
       const unsigned long long target = tk - a + (unsigned long long)nt;
       unsigned polls = 0;
       while (__hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         if (++polls > kFinSpin) {
           __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          vb = -2;
+          vb = kLoopTimeout;
           break;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -2295,8 +2298,8 @@ __device__ __forceinline__ bool scloop_iter(LoopKA* kb, const int t, const unsig
   }
   __syncthreads();
   const int vb = *vbl;
-  mark(vb == -2 ? 9 : 3);
-  if (vb == -2) return false;  // (timed out: leave; the others time out on fin_done)
+  mark(vb == kLoopTimeout ? 9 : 3);
+  if (vb == kLoopTimeout) return false;  // (timed out: leave; the others time out on fin_done)
   if (vb >= 0) {
     cfinish_vb<true>(vb, red, sc, sh3, QSC_LA(slab), nt, nks, R, QSC_LA(K), QSC_LA(C), 1,
                      nullptr, QSC_LA(mC), QSC_LA(vC), QSC_LA(adc), QSC_LA(lambda_c), nullptr,
