@@ -524,6 +524,35 @@ def test_fused_finish_is_bitexact(n, shape):
         assert st == rs
 
 
+@pytest.mark.parametrize("n", [2, 3, 9])
+@pytest.mark.parametrize("shape", [(8, 192, 192, 256), (8, 384, 384, 256)])
+def test_persistent_loop_is_bitexact(n, shape):
+    """qsc_scpass_loop (the n - 1 fused bodies with their C-finish in ONE persistent launch, a
+    device-wide wait on the workspace's completed-items counter between bodies, include/qsc.h)
+    gives the launch pairs' S, C, moments, history and state bit for bit, eager and hipGraph,
+    with every counter where it should be (tickets and C-finish items of every iteration)."""
+    from quantized_spectrum_cartography_amd.obs import Observations
+    from quantized_spectrum_cartography_amd.qmc import FreeSSolver
+    R, I, J, K = shape
+    d = _random_case(58, R, I, J, K)
+    o = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=R, tile=1024)
+    ref = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, fin=False, loop=False)
+    ref.run(n)
+    nvb = R * o.desc.nks + 2
+    for g in (False, True):
+        sol = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, loop=True)
+        assert sol.loop, "the persistent loop does not apply at this shape"
+        sol.run(n, use_graph=g)
+        for x, y in ((ref.S, sol.S), (ref.C, sol.C), (ref.mS, sol.mS), (ref.vS, sol.vS),
+                     (ref.mC, sol.mC), (ref.vC, sol.vC)):
+            assert torch.equal(x, y)
+        assert ref.history() == sol.history()
+        st, rs = sol.state(), ref.state()
+        assert st["fused_fault"] == 0
+        assert st == rs
+        assert sol.engine.fin_counters() == ((n - 1) * o.desc.ntiles, (n - 1) * nvb)
+
+
 @pytest.mark.parametrize("log_model,R,I,J,K,s_scale,lr_s,n", [
     (True, 4, 32, 32, 16, None, 0.1, 3),        # log model: 0.5 % of S projected
     (False, 8, 64, 64, 256, 0.02, 0.05, 6)])   # one-bit, fused launches
