@@ -17,25 +17,74 @@ from .qmc import _solve_generator
 from .utils import LOG_OFFSET_7_ADJUSTED as LOG_OFFSET
 
 
-def make_decoder(I, J, zdim=256, seed=0):
+def make_decoder(I, J, zdim=256, seed=0, ndf=16):
+    """A DIP decoder for I x J maps: the reference's DecoderDip at 51 x 51 (zdim 256, ndf 16),
+    SizedDecoderDip otherwise (`ndf` sets its widths; 16 is the reference's)."""
     if I != J:
         raise ValueError("the DIP decoder produces square maps")
     g = torch.Generator().manual_seed(seed)
     with torch.random.fork_rng(devices=[]):
         torch.manual_seed(int(torch.randint(0, 2 ** 31 - 1, (1,), generator=g)))
-        net = DecoderDip() if (I == 51 and zdim == 256) else SizedDecoderDip(I, zdim)
+        net = (DecoderDip() if (I == 51 and zdim == 256 and ndf == 16)
+               else SizedDecoderDip(I, zdim, ndf=ndf))
     return net
+
+
+@torch.no_grad()
+def calibrate_bn(decoder, Z):
+    """Data-dependent initialisation of the decoder's BatchNorm layers: their running statistics
+    set to the batch statistics of one forward pass at Z (train mode, momentum 1), then eval
+    mode.  A freshly initialised decoder run in eval mode (unit running variance) lets the
+    activations of its ~16 conv layers drift far from unit scale and the output sigmoid
+    saturate, where a pre-fit to a warm start no longer moves it; after calibration every BN
+    layer normalises the activations Z actually produces, and the R emitters still decode
+    independently (eval mode)."""
+    bns = [m for m in decoder.modules() if isinstance(m, torch.nn.modules.batchnorm._BatchNorm)]
+    saved = [(m.momentum, m.training) for m in bns]
+    decoder.train()
+    for m in bns:
+        m.reset_running_stats()
+        m.momentum = 1.0
+    decoder(Z)
+    for m, (mom, _) in zip(bns, saved):
+        m.momentum = mom
+    decoder.eval()
+    return decoder
+
+
+def prefit(decoder, Z, S_target, steps=1000, lr=1e-2, peak=0.9):
+    """Fit the decoder's output to a warm-start S (e.g. warm.warm_start), fields scaled to
+    `peak` at their maximum (the sigmoid output's range).  Returns the scale s: the decoder then
+    represents S_target / s, so C_init * s keeps T_hat = S C."""
+    R = S_target.shape[0]
+    I, J = S_target.shape[-2], S_target.shape[-1]
+    S_target = S_target.detach().to(Z.device, torch.float32).reshape(R, 1, I, J)
+    s = float(S_target.max()) / peak if float(S_target.max()) > 0 else 1.0
+    target = (S_target / s).clamp(1e-4, peak)
+    opt = torch.optim.Adam(decoder.parameters(), lr=lr)
+    for _ in range(int(steps)):
+        opt.zero_grad()
+        loss = torch.nn.functional.mse_loss(decoder(Z).reshape(R, 1, I, J), target)
+        loss.backward()
+        opt.step()
+    return s
 
 
 def solve(Y, Wx, bin_boundaries, noise_std, R, offset=None, log_model=True, decoder=None,
           Z_init=None, C_init=None, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
           max_iter=500, optimize="weights", T_true=None, nmse_every=0, obs=None, tile=None,
-          seed=0, callback=None):
+          seed=0, callback=None, S_init=None, prefit_steps=1000, prefit_lr=1e-2, ndf=16):
     """DIP-regularised alternating probit MLE (config 5: log model + DIP prior on S).
 
     `offset` defaults to the reference log model's LOG_OFFSET_7_ADJUSTED
     (qmc/quantization_model_log.py:7, 9): with the zero C_init the first C-pass sees
-    T_hat = 0, and log(0 + offset) must stay finite."""
+    T_hat = 0, and log(0 + offset) must stay finite.
+
+    Warm start (the notebook's optional warm start, qmc/qmc.ipynb :513-516): with S_init (R,1,I,J)
+    and C_init (e.g. warm.warm_start), a decoder built here is BN-calibrated at Z, pre-fitted to
+    S_init (`prefit_steps` Adam steps at `prefit_lr`), and C_init rescaled by the pre-fit's
+    field scale, so the solve starts from the warm start's map.  A fresh decoder is always
+    BN-calibrated (calibrate_bn)."""
     if log_model:
         offset = LOG_OFFSET if offset is None else float(offset)
         if not offset > 0.0:
@@ -46,14 +95,24 @@ def solve(Y, Wx, bin_boundaries, noise_std, R, offset=None, log_model=True, deco
         obs = Observations(Y, Wx, bin_boundaries, noise_std, offset=offset if log_model else 0.0,
                            log_model=log_model, tile=tile, R_hint=R)
     dev = obs.device
-    if decoder is None:
-        decoder = make_decoder(I, J, seed=seed)
+    fresh = decoder is None
+    if fresh:
+        decoder = make_decoder(I, J, seed=seed, ndf=ndf)
     decoder = decoder.to(dev).eval()
     if Z_init is None:
         g = torch.Generator().manual_seed(seed + 1)
         Z_init = torch.randn((R, 256), generator=g)
     if C_init is None:
         C_init = torch.zeros(R, K)
+    if fresh:
+        calibrate_bn(decoder, Z_init.detach().to(dev, torch.float32))
+    if S_init is not None:
+        if not fresh:
+            raise ValueError("S_init pre-fits the decoder built here; pass decoder=None")
+        scale = prefit(decoder, Z_init.detach().to(dev, torch.float32), S_init,
+                       steps=prefit_steps, lr=prefit_lr)
+        C_init = C_init.detach().to(torch.float32) * scale
+        decoder.eval()
     for p in decoder.parameters():
         p.requires_grad_(optimize in ("weights", "both"))
     params = []

@@ -20,9 +20,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=500)
     ap.add_argument("--prefit", type=int, default=2000)
+    ap.add_argument("--prefit-marks", type=int, nargs="*", default=[250, 1000])
+    ap.add_argument("--ndf", type=int, nargs="*", default=[16, 64])
     ap.add_argument("--prefit-lr", type=float, default=1e-2)
     ap.add_argument("--seed", type=int, default=5)
-    ap.add_argument("--free-scales", type=float, nargs="*", default=[1e-3, 3e-3, 1e-2])
+    ap.add_argument("--free-scales", type=float, nargs="*", default=[1e-2, 3e-2])
     ap.add_argument("--dip-lr-s", type=float, nargs="*", default=[1e-4, 1e-3])
     ap.add_argument("--dip-lr-c-scale", type=float, default=1e-3)
     args = ap.parse_args()
@@ -62,40 +64,43 @@ def main():
             "traj": tr[:: max(1, len(tr) // 10)], "best": min(tr, key=lambda x: x[1]),
             "final_lin_log": pair(rf.S, rf.C), "finite": bool(torch.isfinite(rf.S).all()),
             "wall_s": round(time.perf_counter() - t0, 2)})
-    # DIP: decoder pre-fitted to the warm-start fields (sigmoid output, fields scaled to 0.9 peak)
-    smax = float(S0.max())
-    target = (S0 / smax * 0.9).reshape(R, 1, N, N).clamp(1e-4, 0.9)
-    dec = dip.make_decoder(N, N, seed=args.seed).cuda().train(False)
+    # DIP from the warm start: a BN-calibrated decoder (dip.calibrate_bn) pre-fitted to the
+    # warm-start fields (dip.prefit), C_init rescaled by the pre-fit scale, then dip.solve
     Z = torch.randn((R, 256), generator=torch.Generator().manual_seed(args.seed + 1)).cuda()
-    opt = torch.optim.Adam(dec.parameters(), lr=args.prefit_lr)
-    C_init = C0 * (smax / 0.9)
-    t0 = time.perf_counter()
-    marks = {}
-    for it in range(1, args.prefit + 1):
-        opt.zero_grad()
-        loss = torch.nn.functional.mse_loss(dec(Z).reshape(R, 1, N, N), target)
-        loss.backward()
-        opt.step()
-        if it in (100, 250, 500, 1000, 2000, 4000) or it == args.prefit:
-            with torch.no_grad():
-                marks[it] = pair(dec(Z).reshape(R, 1, N, N), C_init) + (round(float(loss), 6),)
-    emit("dip_prefit", {"lr": args.prefit_lr, "marks_lin_log_mse": marks,
-                        "wall_s": round(time.perf_counter() - t0, 2)})
-    state = {k: v.clone() for k, v in dec.state_dict().items()}
-    for lr_s in args.dip_lr_s:
-        dec.load_state_dict(state)
+    for ndf in args.ndf:
+        dec = dip.make_decoder(N, N, seed=args.seed, ndf=ndf).cuda()
+        dip.calibrate_bn(dec, Z)
+        with torch.no_grad():
+            out0 = dec(Z)
         t0 = time.perf_counter()
-        rd = dip.solve(Y, Wx, b, 5.0, R, offset=off, max_iter=args.iters, decoder=dec, Z_init=Z,
-                       C_init=C_init.cpu(), lr_c=args.dip_lr_c_scale * float(C_init.abs().mean()),
-                       lr_s=lr_s, T_true=T, nmse_every=25)
-        torch.cuda.synchronize()
-        tr = [[25 * (i + 1), round(float(v), 5)] for i, v in enumerate(rd.nmse)]
-        emit("dip_lr_s%g" % lr_s, {
-            "lr_s": lr_s, "lr_c": args.dip_lr_c_scale * float(C_init.abs().mean()),
-            "iters": args.iters, "traj": tr, "best": min(tr, key=lambda x: x[1]) if tr else None,
-            "final_lin_log": pair(rd.S, rd.C), "finite": bool(torch.isfinite(rd.S).all()),
-            "wall_s": round(time.perf_counter() - t0, 2)})
-
+        marks = {}
+        done = 0
+        scale = None
+        for mark in sorted(set(args.prefit_marks + [args.prefit])):
+            scale = dip.prefit(dec, Z, S0, steps=mark - done, lr=args.prefit_lr)
+            done = mark
+            dec.eval()
+            with torch.no_grad():
+                marks[mark] = pair(dec(Z).reshape(R, 1, N, N), C0 * scale)
+        emit("dip_prefit_ndf%d" % ndf, {"lr": args.prefit_lr, "out0_range": [float(out0.min()), float(out0.max())],
+                                        "marks_lin_log": marks, "wall_s": round(time.perf_counter() - t0, 2)})
+        state = {k: v.clone() for k, v in dec.state_dict().items()}
+        C_init = C0 * scale
+        for lr_s in args.dip_lr_s:
+            dec.load_state_dict(state)
+            dec.eval()
+            t0 = time.perf_counter()
+            lr_c = args.dip_lr_c_scale * float(C_init.abs().mean())
+            rd = dip.solve(Y, Wx, b, 5.0, R, offset=off, max_iter=args.iters, decoder=dec,
+                           Z_init=Z, C_init=C_init.cpu(), lr_c=lr_c, lr_s=lr_s, T_true=T,
+                           nmse_every=25)
+            torch.cuda.synchronize()
+            tr = [[25 * (i + 1), round(float(v), 5)] for i, v in enumerate(rd.nmse)]
+            emit("dip_ndf%d_lr_s%g" % (ndf, lr_s), {
+                "lr_s": lr_s, "lr_c": lr_c, "iters": args.iters, "traj": tr,
+                "best": min(tr, key=lambda x: x[1]) if tr else None,
+                "final_lin_log": pair(rd.S, rd.C), "finite": bool(torch.isfinite(rd.S).all()),
+                "wall_s": round(time.perf_counter() - t0, 2)})
 
 if __name__ == "__main__":
     main()
