@@ -73,18 +73,27 @@ def prefit(decoder, Z, S_target, steps=1000, lr=1e-2, peak=0.9):
 def solve(Y, Wx, bin_boundaries, noise_std, R, offset=None, log_model=True, decoder=None,
           Z_init=None, C_init=None, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
           max_iter=500, optimize="weights", T_true=None, nmse_every=0, obs=None, tile=None,
-          seed=0, callback=None, S_init=None, prefit_steps=1000, prefit_lr=1e-2, ndf=16):
+          seed=0, callback=None, S_init=None, prefit_steps=1000, prefit_lr=1e-2, ndf=16,
+          warm="residual", residual_scale=None):
     """DIP-regularised alternating probit MLE (config 5: log model + DIP prior on S).
 
     `offset` defaults to the reference log model's LOG_OFFSET_7_ADJUSTED
     (qmc/quantization_model_log.py:7, 9): with the zero C_init the first C-pass sees
     T_hat = 0, and log(0 + offset) must stay finite.
 
-    Warm start (the notebook's optional warm start, qmc/qmc.ipynb :513-516): with S_init (R,1,I,J)
-    and C_init (e.g. warm.warm_start), a decoder built here is BN-calibrated at Z, pre-fitted to
-    S_init (`prefit_steps` Adam steps at `prefit_lr`), and C_init rescaled by the pre-fit's
-    field scale, so the solve starts from the warm start's map.  A fresh decoder is always
-    BN-calibrated (calibrate_bn)."""
+    Warm start (the notebook's optional warm start, qmc/qmc.ipynb :513-516), S_init (R,1,I,J)
+    and C_init (e.g. warm.warm_start):
+      warm="residual" (default): S = max(S_init + a (D(Z) - D(Z_0)), 0) with D(Z_0) the
+        decoder's output at the start (a constant): the solve starts exactly at the warm
+        start's map and the decoder parameterises the correction, a DIP prior on the update
+        (a = residual_scale, default the warm-start fields' mean absolute value);
+      warm="relative": S = S_init exp(a (D(Z) - D(Z_0))) (a default 1): the correction is
+        relative, so S stays > 0 wherever S_init is and small values keep their scale (the log
+        model's domain);
+      warm="prefit": the decoder itself is pre-fitted to S_init (`prefit_steps` Adam steps at
+        `prefit_lr`) and C_init rescaled by the pre-fit's field scale (a 256 x 256 decoder of
+        the reference's widths cannot reproduce the fields' peaks: profiles/r04/c5_explore*).
+    A fresh decoder is always BN-calibrated (calibrate_bn)."""
     if log_model:
         offset = LOG_OFFSET if offset is None else float(offset)
         if not offset > 0.0:
@@ -106,21 +115,53 @@ def solve(Y, Wx, bin_boundaries, noise_std, R, offset=None, log_model=True, deco
         C_init = torch.zeros(R, K)
     if fresh:
         calibrate_bn(decoder, Z_init.detach().to(dev, torch.float32))
-    if S_init is not None:
+    net = decoder
+    if S_init is not None and warm == "prefit":
         if not fresh:
-            raise ValueError("S_init pre-fits the decoder built here; pass decoder=None")
+            raise ValueError("warm='prefit' pre-fits the decoder built here; pass decoder=None")
         scale = prefit(decoder, Z_init.detach().to(dev, torch.float32), S_init,
                        steps=prefit_steps, lr=prefit_lr)
         C_init = C_init.detach().to(torch.float32) * scale
         decoder.eval()
+    elif S_init is not None:
+        if warm not in ("residual", "relative"):
+            raise ValueError("warm must be 'residual', 'relative' or 'prefit'")
+        base = S_init.detach().to(dev, torch.float32).reshape(R, 1, I, J)
+        if warm == "residual":
+            a = float(base.abs().mean()) if residual_scale is None else float(residual_scale)
+        else:
+            a = 1.0 if residual_scale is None else float(residual_scale)
+        with torch.no_grad():
+            d0 = decoder(Z_init.detach().to(dev, torch.float32)).reshape(R, 1, I, J).clone()
+        net = _Residual(decoder, base, d0, a, relative=warm == "relative")
     for p in decoder.parameters():
         p.requires_grad_(optimize in ("weights", "both"))
     params = []
     if optimize in ("weights", "both"):
         params += list(decoder.parameters())
     Zp = Z_init.detach().to(dev, torch.float32).clone()
-    res = _solve_generator(obs, decoder, Zp, C_init, R, lambda_c, lambda_s, lr_c, lr_s, max_iter,
+    res = _solve_generator(obs, net, Zp, C_init, R, lambda_c, lambda_s, lr_c, lr_s, max_iter,
                            (0.9, 0.999), 1e-8, True, False, (0, 0), T_true, nmse_every, callback,
                            params=params, optimize_z=optimize in ("z", "both"))
     res.decoder = decoder
     return res
+
+
+class _Residual(torch.nn.Module):
+    """S = max(base + a (D(Z) - d0), 0) (dip.solve warm="residual") or base exp(a (D(Z) - d0))
+    (warm="relative"): the warm-start map with a decoder-parameterised correction; S >= 0 as the
+    reference's sigmoid-output S."""
+
+    def __init__(self, decoder, base, d0, a, relative=False):
+        super().__init__()
+        self.decoder = decoder
+        self.register_buffer("base", base)
+        self.register_buffer("d0", d0)
+        self.a = a
+        self.relative = relative
+
+    def forward(self, z):
+        d = self.decoder(z).reshape(self.base.shape)
+        if self.relative:
+            return self.base * torch.exp(self.a * (d - self.d0))
+        return torch.clamp_min(self.base + self.a * (d - self.d0), 0.0)

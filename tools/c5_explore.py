@@ -25,7 +25,9 @@ def main():
     ap.add_argument("--prefit-lr", type=float, default=1e-2)
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--free-scales", type=float, nargs="*", default=[1e-2, 3e-2])
-    ap.add_argument("--dip-lr-s", type=float, nargs="*", default=[1e-4, 1e-3])
+    ap.add_argument("--dip-lr-s", type=float, nargs="*", default=[1e-4, 1e-3, 1e-2])
+    ap.add_argument("--dip-lr-c-scales", type=float, nargs="*", default=[1e-2])
+    ap.add_argument("--dip-forms", nargs="*", default=["residual", "relative"])
     ap.add_argument("--dip-lr-c-scale", type=float, default=1e-3)
     args = ap.parse_args()
     from quantized_spectrum_cartography_amd import dip, maps, metrics, qmc, warm
@@ -64,40 +66,19 @@ def main():
             "traj": tr[:: max(1, len(tr) // 10)], "best": min(tr, key=lambda x: x[1]),
             "final_lin_log": pair(rf.S, rf.C), "finite": bool(torch.isfinite(rf.S).all()),
             "wall_s": round(time.perf_counter() - t0, 2)})
-    # DIP from the warm start: a BN-calibrated decoder (dip.calibrate_bn) pre-fitted to the
-    # warm-start fields (dip.prefit), C_init rescaled by the pre-fit scale, then dip.solve
-    Z = torch.randn((R, 256), generator=torch.Generator().manual_seed(args.seed + 1)).cuda()
-    for ndf in args.ndf:
-        dec = dip.make_decoder(N, N, seed=args.seed, ndf=ndf).cuda()
-        dip.calibrate_bn(dec, Z)
-        with torch.no_grad():
-            out0 = dec(Z)
-        t0 = time.perf_counter()
-        marks = {}
-        done = 0
-        scale = None
-        for mark in sorted(set(args.prefit_marks + [args.prefit])):
-            scale = dip.prefit(dec, Z, S0, steps=mark - done, lr=args.prefit_lr)
-            done = mark
-            dec.eval()
-            with torch.no_grad():
-                marks[mark] = pair(dec(Z).reshape(R, 1, N, N), C0 * scale)
-        emit("dip_prefit_ndf%d" % ndf, {"lr": args.prefit_lr, "out0_range": [float(out0.min()), float(out0.max())],
-                                        "marks_lin_log": marks, "wall_s": round(time.perf_counter() - t0, 2)})
-        state = {k: v.clone() for k, v in dec.state_dict().items()}
-        C_init = C0 * scale
-        for lr_s in args.dip_lr_s:
-            dec.load_state_dict(state)
-            dec.eval()
+    # DIP from the warm start, residual form (dip.solve warm="residual"): S = max(S0 + a (D(Z) -
+    # D(Z0)), 0), the decoder weights optimised, C from C0 (lr_c at the warm-start C's scale)
+    for form, lr_s in [(f, l) for f in args.dip_forms for l in args.dip_lr_s]:
+        for cs in args.dip_lr_c_scales:
             t0 = time.perf_counter()
-            lr_c = args.dip_lr_c_scale * float(C_init.abs().mean())
-            rd = dip.solve(Y, Wx, b, 5.0, R, offset=off, max_iter=args.iters, decoder=dec,
-                           Z_init=Z, C_init=C_init.cpu(), lr_c=lr_c, lr_s=lr_s, T_true=T,
-                           nmse_every=25)
+            lr_c = cs * c_mag
+            rd = dip.solve(Y, Wx, b, 5.0, R, offset=off, max_iter=args.iters, S_init=S0.cpu(),
+                           C_init=C0.cpu(), lr_c=lr_c, lr_s=lr_s, T_true=T, nmse_every=25,
+                           seed=args.seed, warm=form)
             torch.cuda.synchronize()
             tr = [[25 * (i + 1), round(float(v), 5)] for i, v in enumerate(rd.nmse)]
-            emit("dip_ndf%d_lr_s%g" % (ndf, lr_s), {
-                "lr_s": lr_s, "lr_c": lr_c, "iters": args.iters, "traj": tr,
+            emit("dip_%s_lr_s%g_c%g" % (form, lr_s, cs), {
+                "lr_s": lr_s, "lr_c": lr_c, "iters": args.iters, "traj": tr[:: max(1, len(tr) // 10)],
                 "best": min(tr, key=lambda x: x[1]) if tr else None,
                 "final_lin_log": pair(rd.S, rd.C), "finite": bool(torch.isfinite(rd.S).all()),
                 "wall_s": round(time.perf_counter() - t0, 2)})

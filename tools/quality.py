@@ -12,8 +12,12 @@ Prints one JSON line of trajectories (map NMSE every few iterations, qmc/quantiz
   c5_*        a generate_map-style radio map (maps.generate_map: Gaussian PSD bumps, path loss x
               FFT-correlated log-normal shadowing, 256 x 256, K = 64, R = 4) quantized with the log
               model as qmc/qmc.ipynb :537 does (4 log bins, LOG_OFFSET_4, sigma = 5), f = 0.1:
-                c5_dip       the DIP solver (dip.solve: decoder prior on S, C from zero), the
-                             notebook's C5 setting.
+                c5_warm_start  the de-quantized SPA warm start (warm.warm_start);
+                c5_dip       the DIP solver from it (dip.solve warm="relative": S = S0
+                             exp(D(Z) - D(Z0)), decoder weights optimised, C from C0);
+                c5_dip_cold  the DIP solver from zero C (BN-calibrated decoder), the notebook's
+                             cold setting;
+                c5_free_warm_projS_*  free S >= 0 (project_s) from the warm start.
 
   python tools/quality.py [--c2-iters 4000] [--dip-iters 600]
 """
@@ -38,11 +42,13 @@ def main():
     ap.add_argument("--c2-iters", type=int, default=4000)
     ap.add_argument("--dip-iters", type=int, default=600)
     ap.add_argument("--seed", type=int, default=5)
-    ap.add_argument("--warm-iters", type=int, default=300)
+    ap.add_argument("--warm-iters", type=int, default=1000)
     ap.add_argument("--warm-width", type=float, default=8.0)
     ap.add_argument("--warm-lr-s", type=float, default=1e-3)
-    ap.add_argument("--prefit-steps", type=int, default=300)
-    ap.add_argument("--free-lr-scales", type=float, nargs="*", default=[1e-3, 1e-4])
+    ap.add_argument("--dip-warm-iters", type=int, default=3000)
+    ap.add_argument("--dip-lr-s", type=float, default=0.03)
+    ap.add_argument("--dip-lr-c-scale", type=float, default=1e-2)
+    ap.add_argument("--free-lr-scales", type=float, nargs="*", default=[1e-2, 1e-3])
     ap.add_argument("--skip-c2", action="store_true")
     args = ap.parse_args()
     from quantized_spectrum_cartography_amd import dip, maps, metrics, qmc, synthetic
@@ -83,21 +89,23 @@ def main():
                      "sigma": 5.0, "offset": LOG_OFFSET_4,
                      "bins_used": torch.bincount(Y.reshape(-1), minlength=4).tolist()}
     if args.dip_iters:
+        # the DIP solver from a cold start (zero C, BN-calibrated decoder): the notebook's setting
         every = max(1, args.dip_iters // 12)
         t0 = time.perf_counter()
         rd = dip.solve(Y, Wx, b, 5.0, R, offset=LOG_OFFSET_4, max_iter=args.dip_iters,
                        T_true=T, nmse_every=every)
         torch.cuda.synchronize()
         zero = float(metrics.map_nmse(torch.zeros_like(rd.S), rd.C, T, log_offset=LOG_OFFSET_4))
-        out["c5_dip"] = {"iters": args.dip_iters, "wall_s": time.perf_counter() - t0,
-                         "map_nmse": traj(rd, every), "slf_nmse": metrics.slf_nmse(rd.S, S_true),
-                         # NMSE_LOG (qmc/quantization_model_log.py:104-111): the log-domain
-                         # error the log model is fitted in, vs the all-zero map's
-                         "map_nmse_log": float(metrics.map_nmse(rd.S, rd.C, T,
-                                                                log_offset=LOG_OFFSET_4)),
-                         "map_nmse_log_zero_map": zero,
-                         "cost_first": rd.costs_s[0], "cost_last": rd.costs_s[-1]}
-        print(json.dumps({"c5_dip": out["c5_dip"]["map_nmse"][-1]}), file=sys.stderr, flush=True)
+        out["c5_dip_cold"] = {"iters": args.dip_iters, "wall_s": time.perf_counter() - t0,
+                              "map_nmse": traj(rd, every), "slf_nmse": metrics.slf_nmse(rd.S, S_true),
+                              # NMSE_LOG (qmc/quantization_model_log.py:104-111): the log-domain
+                              # error the log model is fitted in, vs the all-zero map's
+                              "map_nmse_log": float(metrics.map_nmse(rd.S, rd.C, T,
+                                                                     log_offset=LOG_OFFSET_4)),
+                              "map_nmse_log_zero_map": zero,
+                              "cost_first": rd.costs_s[0], "cost_last": rd.costs_s[-1]}
+        print(json.dumps({"c5_dip_cold": out["c5_dip_cold"]["map_nmse"][-1]}), file=sys.stderr,
+              flush=True)
     if args.warm_iters:
         out.update(c5_warm_runs(Y, Wx, b, T, S_true, R, args))
     print(json.dumps(out), flush=True)
@@ -110,13 +118,11 @@ def _nmse_pair(S, C, T, off):
 
 def c5_warm_runs(Y, Wx, b, T, S_true, R, args):
     """C5 from the de-quantized SPA warm start (warm.warm_start; the notebook's optional warm
-    start, qmc/qmc.ipynb :513-516): the warm start itself, then the DIP solver with its decoder
-    pre-fitted to the warm-start S and C initialised from the warm-start C (lr_c scaled to C)."""
+    start, qmc/qmc.ipynb :513-516): the warm start itself, the DIP solver from it (relative
+    form) and free S >= 0 from it."""
     from quantized_spectrum_cartography_amd import dip, metrics, warm
     from quantized_spectrum_cartography_amd.utils import LOG_OFFSET_4
     out = {}
-    K = Y.shape[0]
-    N = Y.shape[-1]
     t0 = time.perf_counter()
     S0, C0 = warm.warm_start(Y.cuda(), Wx.cuda(), b, 5.0, R, offset=LOG_OFFSET_4, log_model=True,
                              width=args.warm_width)
@@ -126,62 +132,51 @@ def c5_warm_runs(Y, Wx, b, T, S_true, R, args):
                             "slf_nmse": metrics.slf_nmse(S0, S_true),
                             "wall_s": time.perf_counter() - t0}
     print(json.dumps({"c5_warm_start": [lin, lg]}), file=sys.stderr, flush=True)
-    # DIP decoder pre-fitted to the warm-start fields (sigmoid output: fields scaled to peak 0.9)
-    smax = float(S0.max())
-    target = (S0 / smax * 0.9).reshape(R, 1, N, N).clamp(1e-4, 0.9)
-    dec = dip.make_decoder(N, N, seed=args.seed).cuda().train(False)
-    Z = torch.randn((R, 256), generator=torch.Generator().manual_seed(args.seed + 1)).cuda()
-    opt = torch.optim.Adam(dec.parameters(), lr=1e-3)
-    for _ in range(args.prefit_steps):
-        opt.zero_grad()
-        loss = torch.nn.functional.mse_loss(dec(Z).reshape(R, 1, N, N), target)
-        loss.backward()
-        opt.step()
-    with torch.no_grad():
-        Sd = dec(Z).reshape(R, 1, N, N)
-    C_init = C0 * (smax / 0.9)
-    lin_p, lg_p = _nmse_pair(Sd, C_init, T, LOG_OFFSET_4)
-    every = max(1, args.warm_iters // 12)
-    lr_c = 5e-3 * float(C_init.abs().mean()) / 0.1  # the notebook's lr_c at its C scale (~0.1)
+    s_mag, c_mag = float(S0.abs().mean()), float(C0.abs().mean())
+    # c5_dip: the DIP solver from the warm start (dip.solve warm="relative": S = S0 exp(D(Z) -
+    # D(Z0)), the decoder's weights optimised; C from C0), Adam steps at the warm-start C's
+    # scale for C and lr_s for the decoder weights
+    every = 25
     t0 = time.perf_counter()
-    rd = dip.solve(Y, Wx, b, 5.0, R, offset=LOG_OFFSET_4, max_iter=args.warm_iters, decoder=dec,
-                   Z_init=Z, C_init=C_init.cpu(), lr_c=lr_c, lr_s=args.warm_lr_s,
-                   T_true=T, nmse_every=every)
+    rd = dip.solve(Y, Wx, b, 5.0, R, offset=LOG_OFFSET_4, max_iter=args.dip_warm_iters,
+                   S_init=S0.cpu(), C_init=C0.cpu(), lr_c=args.dip_lr_c_scale * c_mag,
+                   lr_s=args.dip_lr_s, warm="relative", T_true=T, nmse_every=every,
+                   seed=args.seed)
     torch.cuda.synchronize()
     lin_f, lg_f = _nmse_pair(rd.S, rd.C, T, LOG_OFFSET_4)
-    out["c5_dip_warm"] = {"iters": args.warm_iters, "prefit_steps": args.prefit_steps,
-                          "lr_c": lr_c, "lr_s": args.warm_lr_s,
-                          "map_nmse_after_prefit": lin_p, "map_nmse_log_after_prefit": lg_p,
-                          "map_nmse": traj(rd, every),
-                          "map_nmse_best": min(([e * (i + 1), v] for i, v in
-                                                enumerate(rd.nmse) for e in [every]),
-                                               key=lambda x: x[1]) if rd.nmse else None,
-                          "map_nmse_final": lin_f, "map_nmse_log_final": lg_f,
-                          "slf_nmse": metrics.slf_nmse(rd.S, S_true),
-                          "wall_s": time.perf_counter() - t0,
-                          "cost_first": rd.costs_s[0], "cost_last": rd.costs_s[-1]}
-    print(json.dumps({"c5_dip_warm": [lin_f, lg_f]}), file=sys.stderr, flush=True)
-    # free S from the warm start (qmc.solve, log model), Adam steps scaled to the warm-start
-    # fields (lr = scale x mean |S0| / mean |C0|), map NMSE every 10 iterations on the device
+    tr = traj(rd, every)
+    out["c5_dip"] = {"iters": args.dip_warm_iters, "start": "warm (c5_warm_start)",
+                     "form": "relative: S = S0 exp(D(Z) - D(Z0))", "lr_s": args.dip_lr_s,
+                     "lr_c": args.dip_lr_c_scale * c_mag,
+                     "map_nmse": tr[:: max(1, len(tr) // 12)],
+                     "map_nmse_best": min(tr, key=lambda x: x[1]) if tr else None,
+                     "map_nmse_final": lin_f, "map_nmse_log_final": lg_f,
+                     "finite": bool(torch.isfinite(rd.S).all()),
+                     "slf_nmse": metrics.slf_nmse(rd.S, S_true),
+                     "wall_s": time.perf_counter() - t0,
+                     "cost_first": rd.costs_s[0], "cost_last": rd.costs_s[-1]}
+    print(json.dumps({"c5_dip": [lin_f, lg_f]}), file=sys.stderr, flush=True)
+    # free S from the warm start (qmc.solve, log model) with S >= 0 (project_s), Adam steps
+    # scaled to the warm-start fields (lr = scale x mean |S0| / mean |C0|), map NMSE every 10
     from quantized_spectrum_cartography_amd import qmc
-    s_mag, c_mag = float(S0.abs().mean()), float(C0.abs().mean())
     for scale in args.free_lr_scales:
         t0 = time.perf_counter()
         rf = qmc.solve(Y, Wx, b, 5.0, R, S_init=S0.cpu(), C_init=C0.cpu(), offset=LOG_OFFSET_4,
-                       log_model=True, lr_s=scale * s_mag, lr_c=scale * c_mag,
+                       log_model=True, lr_s=scale * s_mag, lr_c=scale * c_mag, project_s=True,
                        max_iter=args.warm_iters, use_graph=True, T_true=T, nmse_every=10)
         torch.cuda.synchronize()
         tr = [[10 * (i + 1), round(float(v), 5)] for i, v in enumerate(rf.nmse)]
         lin_f, lg_f = _nmse_pair(rf.S, rf.C, T, LOG_OFFSET_4)
-        out["c5_free_warm_lr%g" % scale] = {
+        out["c5_free_warm_projS_lr%g" % scale] = {
             "iters": args.warm_iters, "lr_s": scale * s_mag, "lr_c": scale * c_mag,
+            "project_s": True,
             "map_nmse": tr[:: max(1, len(tr) // 12)], "map_nmse_best": min(tr, key=lambda x: x[1]),
             "map_nmse_final": lin_f, "map_nmse_log_final": lg_f,
-            "slf_nmse": (metrics.slf_nmse(rf.S, S_true) if bool(torch.isfinite(rf.S).all())
-                         else None),  # (free S can leave T_hat + offset <= 0: log of it NaN)
+            "finite": bool(torch.isfinite(rf.S).all()),
+            "slf_nmse": metrics.slf_nmse(rf.S, S_true),
             "wall_s": time.perf_counter() - t0,
             "cost_first": rf.costs_s[0], "cost_last": rf.costs_s[-1]}
-        print(json.dumps({"c5_free_warm_lr%g" % scale: [lin_f, lg_f]}), file=sys.stderr,
+        print(json.dumps({"c5_free_warm_projS_lr%g" % scale: [lin_f, lg_f]}), file=sys.stderr,
               flush=True)
     return out
 
