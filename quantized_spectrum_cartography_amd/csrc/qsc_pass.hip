@@ -1457,6 +1457,18 @@ size_t cpass_tile_lds(int PT, int R, int nks, int NP, bool sr) {
 // finishing workgroups on other XCDs see them once the stores have completed (s_waitcnt) --
 // no L2 write-back fence per workgroup (measured: with one `buffer_wbl2` per workgroup the
 // launch took 40 us against 31 + 3 for the launch pair).  Without FIN: plain stores.
+// ... and their loads in the finishing workgroups: agent-scope relaxed atomic loads (sc1, served
+// by the XCD's L2, never by the CU's L1), so that with write-through stores on the producer side
+// and the vmcnt-drained ticket no acquire fence is needed (MI355X_MICROARCH.md, hand-off forms:
+// every load of the handed-off bytes sc1, every store sc1, one lane signalling behind a barrier)
+template <bool FIN, typename T>
+__device__ __forceinline__ T ld_fin(const T* p) {
+  if constexpr (FIN)
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    return *p;
+}
+
 template <bool FIN, typename T>
 __device__ __forceinline__ void st_fin(T* p, T v) {
   if constexpr (FIN)
@@ -1970,11 +1982,11 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
 
   // ||C||^2 of the C this step differentiates: written by the C-pass (C is read-only there),
   // or the caller's global value (K-slab); never re-read here, where blocks overwrite C
-  const float nsq = normsq_ext ? *normsq_ext : *cnsq;
+  const float nsq = normsq_ext ? *normsq_ext : ld_fin<DEV>(cnsq);
 
   if (vb == R * nks + 1) {
     // the next C-step's Adam scalars (the next S-pass settles step_c + 1 in between)
-    if (mode == 1 && threadIdx.x == 0) adam_cache_store<DEV>(acache, ad, st->step_c + 2);
+    if (mode == 1 && threadIdx.x == 0) adam_cache_store<DEV>(acache, ad, ld_fin<DEV>(&st->step_c) + 2);
     return;
   }
   if (vb == R * nks) {
@@ -1982,7 +1994,7 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
     // Every partial is read up front (one memory round trip, batches of 8 loads in flight)
     // and the three fixed-order block sums share one LDS pass; same sums, same order as
     // settle_s + block_sum.
-    const int pend = st->pending;
+    const int pend = ld_fin<DEV>(&st->pending);
     const bool settle = (pend & (QSC_PEND_SNLL | QSC_PEND_SUPD)) != 0;
     const bool supd = (pend & QSC_PEND_SUPD) != 0;
     float a = 0.0f, b = 0.0f, c = 0.0f;
@@ -1992,8 +2004,8 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int i = min(i0 + j * step, nslices - 1);
-        va[j] = part_nll_s[i];
-        vb[j] = supd ? part_nsq_s[i] : 0.0f;
+        va[j] = ld_fin<DEV>(&part_nll_s[i]);
+        vb[j] = supd ? ld_fin<DEV>(&part_nsq_s[i]) : 0.0f;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j)
@@ -2002,7 +2014,7 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
           if (supd) b += vb[j];
         }
     }
-    for (int i = threadIdx.x; i < npart_c; i += blockDim.x) c += part_nll_c[i];
+    for (int i = threadIdx.x; i < npart_c; i += blockDim.x) c += ld_fin<DEV>(&part_nll_c[i]);
     a = wave_sum(a);
     b = wave_sum(b);
     c = wave_sum(c);
@@ -2021,17 +2033,17 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
       }
       int pnd = pend;
       if (settle) {  // settle_s, thread-0 part
-        const int it = st->iter - 1;
+        const int it = ld_fin<DEV>(&st->iter) - 1;
         st_fin<DEV>(&st->nll_s, sn);
         if (hist && it >= 0 && it < hist_cap) {
-          hist[4 * it + 0] = st->nll_c;
+          hist[4 * it + 0] = ld_fin<DEV>(&st->nll_c);
           hist[4 * it + 1] = sn;
-          hist[4 * it + 2] = st->normsq_c;
-          hist[4 * it + 3] = st->normsq_s_prev;
+          hist[4 * it + 2] = ld_fin<DEV>(&st->normsq_c);
+          hist[4 * it + 3] = ld_fin<DEV>(&st->normsq_s_prev);
         }
         if (supd) {
           st_fin<DEV>(&st->normsq_s, sq);
-          st_fin<DEV>(&st->step_s, st->step_s + 1);
+          st_fin<DEV>(&st->step_s, ld_fin<DEV>(&st->step_s) + 1);
         }
         pnd = pend & ~(QSC_PEND_SNLL | QSC_PEND_SUPD);
         st_fin<DEV>(&st->pending, pnd);
@@ -2058,7 +2070,7 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
   }
   if (threadIdx.x == 0 && mode == 1) {
     const AdamCache a0 = acache[0], a1 = acache[1];  // both slots: no dependent read on step_c
-    const int step = st->step_c + 1;
+    const int step = ld_fin<DEV>(&st->step_c) + 1;
     const float nrm = sqrtf(nsq);
     sc.coef = nrm > 0.0f ? lambda_c / nrm : 0.0f;
     sc.as = adam_scalars_cached((step & 1) ? a1 : a0, ad, step);
@@ -2072,7 +2084,7 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int tt = t0 + j * NW;
-      v[j] = col[(int64_t)min(tt, ntiles - 1) * tstride];
+      v[j] = ld_fin<DEV>(&col[(int64_t)min(tt, ntiles - 1) * tstride]);
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j)
@@ -2172,7 +2184,9 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
         }
         __builtin_amdgcn_s_sleep(2);
       }
-      if (vb >= 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      // (no acquire fence: every value the C-finish item reads from this launch's other
+      // workgroups is loaded sc1, ld_fin; C, mC, vC and the C-side Adam cache are from the
+      // previous launch)
     }
     *vbl = vb;
   }
@@ -2181,9 +2195,9 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
   __syncthreads();
   const int vb = *vbl;
   if (vb < 0) return;
-  cfinish_vb(vb, red, sc, sh3, slab, nt, nks, R, K, C, 1, nullptr, mC, vC, adc, lambda_c,
-             nullptr, cnsq, st, part_nll_c, nt * nks, part_nll_s, part_nsq_s,
-             nt * PT / QSC_SLICE, hist, hist_cap, acache_c);
+  cfinish_vb<true>(vb, red, sc, sh3, slab, nt, nks, R, K, C, 1, nullptr, mC, vC, adc, lambda_c,
+                   nullptr, cnsq, st, part_nll_c, nt * nks, part_nll_s, part_nsq_s,
+                   nt * PT / QSC_SLICE, hist, hist_cap, acache_c);
   STAMP(wg, 21);  // C-finish item done
 }
 
