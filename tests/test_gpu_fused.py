@@ -270,6 +270,37 @@ def test_dip_solver_256():
     assert np.all(np.isfinite(res.costs_c))
 
 
+@pytest.mark.parametrize("warm", ["relative", "residual"])
+def test_dip_warm_start_forms(warm):
+    """dip.solve from a warm start (S_init, C_init): the first S-step sees exactly the warm
+    start's S (the decoder enters only through D(Z) - D(Z0), zero at the start), S stays >= 0,
+    and the run stays finite; a BN-calibrated fresh decoder's output is not saturated."""
+    from quantized_spectrum_cartography_amd import dip
+    from quantized_spectrum_cartography_amd.utils import QUANTIZATION_BOUNDARIES_4_BINS_LOG
+    torch.manual_seed(2)
+    R, K, N = 2, 8, 64
+    S_true = torch.rand(R, 1, N, N) * 0.2
+    C_true = torch.rand(R, K)
+    Tt = ro.get_tensor(S_true, C_true)
+    b = torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG)
+    Y = ro.quantize(Tt, 5.0, b, offset=1e-10, log_model=True).unsqueeze(1)
+    Wx = torch.bernoulli(torch.full((K, 1, N, N), 0.1))
+    S0 = S_true * (1.0 + 0.1 * torch.rand(R, 1, N, N))
+    seen = []
+    res = dip.solve(Y, Wx, b, 5.0, R, offset=1e-10, max_iter=5, S_init=S0, C_init=C_true,
+                    lr_s=1e-3, lr_c=1e-3, warm=warm,
+                    callback=lambda i, d: seen.append(d["S"].detach().cpu().clone()))
+    assert torch.allclose(seen[0], S0, rtol=1e-6, atol=0)
+    assert bool((res.S >= 0).all()) and np.all(np.isfinite(res.costs_c))
+    assert np.all(np.isfinite(res.costs_s))
+    dec = dip.make_decoder(N, N, seed=0).cuda()
+    z = torch.randn(R, 256, device="cuda")
+    dip.calibrate_bn(dec, z)
+    with torch.no_grad():
+        out = dec(z)
+    assert float(out.std()) > 1e-3 and 0.0 < float(out.mean()) < 1.0
+
+
 @pytest.mark.parametrize("seed,R,I,J,K,log_model,tile", [
     (31, 4, 32, 32, 16, True, None),     # log model (qmc_dowjons.ipynb form)
     (32, 8, 64, 64, 128, True, 512),     # rank 8, two k-slices
