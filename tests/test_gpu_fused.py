@@ -290,7 +290,9 @@ def test_dip_warm_start_forms(warm):
     res = dip.solve(Y, Wx, b, 5.0, R, offset=1e-10, max_iter=5, S_init=S0, C_init=C_true,
                     lr_s=1e-3, lr_c=1e-3, warm=warm,
                     callback=lambda i, d: seen.append(d["S"].detach().cpu().clone()))
-    assert torch.allclose(seen[0], S0, rtol=1e-6, atol=0)
+    # (two calls of the decoder at the same Z may differ in the last bits: MIOpen's algorithm
+    # choice, so D(Z) - D(Z0) is ~1e-7, not exactly 0, at the start)
+    assert torch.allclose(seen[0], S0, rtol=1e-5, atol=1e-6 * float(S0.abs().mean()))
     assert bool((res.S >= 0).all()) and np.all(np.isfinite(res.costs_c))
     assert np.all(np.isfinite(res.costs_s))
     dec = dip.make_decoder(N, N, seed=0).cuda()
