@@ -38,6 +38,11 @@ constexpr int kSWaves = kSBlock / 64;
 #define QSC_CPASS_BLOCK 512
 #endif
 constexpr int kCBlock = QSC_CPASS_BLOCK;  // C-pass: kCBlock/64 waves = parts of one (tile, 64-bin slice)
+// C-pass tile form: a bin list is split into parts while each part keeps at least this many
+// 4-entry chunks (every C-pass form and the fused launches share the partition)
+#ifndef QSC_CPART_MIN_CHUNKS
+#define QSC_CPART_MIN_CHUNKS 3.0
+#endif
 constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 
 // occupancy targets (waves per SIMD) that bound the register allocation of the passes; the
@@ -1972,11 +1977,16 @@ __device__ void settle_s(qsc_state* __restrict__ st, const float* __restrict__ p
 constexpr int kFWaves = kFBlock / 64;
 
 // C-finish work item vb of R*nks + 2 (cfinish_kernel: vb = the workgroup; scfin_kernel: one
-// item per late-arriving workgroup), with its LDS scratch passed in
+// item per late-arriving workgroup), with its LDS scratch passed in.  The sums are those of a
+// 16-wave workgroup (kFWaves partial sums per column, in wave order); a smaller workgroup (the
+// fused finish of a 4..15-wave fused launch, DEV) runs them as virtual waves vw = wave,
+// wave + NWp, ... (at most VF per physical wave), same operands in the same order.
 template <bool DEV = false>
 __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scalars& sc,
                                            float (*sh3)[kFWaves], QSC_CF_PARAMS) {
   constexpr int NW = kFWaves;
+  constexpr int VF = DEV ? 4 : 1;  // virtual waves per physical wave (>= 4 physical waves)
+  const int NWp = DEV ? (int)(blockDim.x >> 6) : NW;
   const int Kp = nks * 64;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 
@@ -1997,31 +2007,34 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
     const int pend = ld_fin<DEV>(&st->pending);
     const bool settle = (pend & (QSC_PEND_SNLL | QSC_PEND_SUPD)) != 0;
     const bool supd = (pend & QSC_PEND_SUPD) != 0;
-    float a = 0.0f, b = 0.0f, c = 0.0f;
-    const int step = blockDim.x;
-    for (int i0 = threadIdx.x; settle && i0 < nslices; i0 += 8 * step) {
-      float va[8], vb[8];
+    constexpr int step = kFBlock;
+    for (int vw = wave; vw < NW; vw += NWp) {
+      const int vt = vw * 64 + lane;
+      float a = 0.0f, b = 0.0f, c = 0.0f;
+      for (int i0 = vt; settle && i0 < nslices; i0 += 8 * step) {
+        float va[8], vb[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int i = min(i0 + j * step, nslices - 1);
-        va[j] = ld_fin<DEV>(&part_nll_s[i]);
-        vb[j] = supd ? ld_fin<DEV>(&part_nsq_s[i]) : 0.0f;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (i0 + j * step < nslices) {
-          a += va[j];
-          if (supd) b += vb[j];
+        for (int j = 0; j < 8; ++j) {
+          const int i = min(i0 + j * step, nslices - 1);
+          va[j] = ld_fin<DEV>(&part_nll_s[i]);
+          vb[j] = supd ? ld_fin<DEV>(&part_nsq_s[i]) : 0.0f;
         }
-    }
-    for (int i = threadIdx.x; i < npart_c; i += blockDim.x) c += ld_fin<DEV>(&part_nll_c[i]);
-    a = wave_sum(a);
-    b = wave_sum(b);
-    c = wave_sum(c);
-    if (lane == 0) {
-      sh3[0][wave] = a;
-      sh3[1][wave] = b;
-      sh3[2][wave] = c;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (i0 + j * step < nslices) {
+            a += va[j];
+            if (supd) b += vb[j];
+          }
+      }
+      for (int i = vt; i < npart_c; i += step) c += ld_fin<DEV>(&part_nll_c[i]);
+      a = wave_sum(a);
+      b = wave_sum(b);
+      c = wave_sum(c);
+      if (lane == 0) {
+        sh3[0][vw] = a;
+        sh3[1][vw] = b;
+        sh3[2][vw] = c;
+      }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2075,22 +2088,35 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
     sc.coef = nrm > 0.0f ? lambda_c / nrm : 0.0f;
     sc.as = adam_scalars_cached((step & 1) ? a1 : a0, ad, step);
   }
-  // tile sum: wave w takes tiles w, w+16, ...; sixteen independent loads in flight per group
+  // tile sum: (virtual) wave w takes tiles w, w+16, ...; sixteen independent loads in flight
+  // per group and virtual wave, the virtual waves' groups issued together
   const float* col = slab + (int64_t)r * Kp + k;
   const int64_t tstride = (int64_t)R * Kp;
-  float a = 0.0f;
-  for (int t0 = wave; t0 < ntiles; t0 += 16 * NW) {
-    float v[16];
+  float a[VF];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int tt = t0 + j * NW;
-      v[j] = ld_fin<DEV>(&col[(int64_t)min(tt, ntiles - 1) * tstride]);
+  for (int f = 0; f < VF; ++f) a[f] = 0.0f;
+  for (int tg = 0; tg < ntiles; tg += 16 * NW) {
+    float v[VF][16];
+#pragma unroll
+    for (int f = 0; f < VF; ++f) {
+      const int vw = wave + f * NWp;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int tt = tg + vw + j * NW;
+        v[f][j] = vw < NW ? ld_fin<DEV>(&col[(int64_t)min(tt, ntiles - 1) * tstride]) : 0.0f;
+      }
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (t0 + j * NW < ntiles) a += v[j];
+    for (int f = 0; f < VF; ++f) {
+      const int vw = wave + f * NWp;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (vw < NW && tg + vw + j * NW < ntiles) a[f] += v[f][j];
+    }
   }
-  red[wave][lane] = a;
+#pragma unroll
+  for (int f = 0; f < VF; ++f)
+    if (wave + f * NWp < NW) red[wave + f * NWp][lane] = a[f];
   __syncthreads();
   if (wave == 0 && k < K) {
     float g = red[0][lane];
@@ -2843,7 +2869,7 @@ static int cpass_impl(const qsc_obs_desc* d, const void* c_entries, const int32_
     const int nks = d->nks;
     int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
     const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
-    while (NP > 1 && chunks / NP < 3.0) --NP;
+    while (NP > 1 && chunks / NP < QSC_CPART_MIN_CHUNKS) --NP;
     const int U = nks * NP;
     const size_t tshm = cpass_tile_lds(d->PT, R, nks, NP, sr);
     if (U >= 4 && tshm <= 160 * 1024) {
@@ -2879,7 +2905,7 @@ static int cpass_parts(const qsc_obs_desc* d, int R, bool sr) {
   const int nks = d->nks;
   int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
   const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
-  while (NP > 1 && chunks / NP < 3.0) --NP;
+  while (NP > 1 && chunks / NP < QSC_CPART_MIN_CHUNKS) --NP;
   const bool tile = QSC_CPASS_TILE && nks * NP >= 4 &&
                     cpass_tile_lds(d->PT, R, nks, NP, sr) <= 160 * 1024;
   return tile ? NP : kCParts;
@@ -2908,7 +2934,7 @@ static bool sr_layout_ok(const qsc_obs_desc* d, int R) {
   const int nks = d->nks;
   int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
   const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
-  while (NP > 1 && chunks / NP < 3.0) --NP;
+  while (NP > 1 && chunks / NP < QSC_CPART_MIN_CHUNKS) --NP;
   const bool tile = QSC_CPASS_TILE && nks * NP >= 4 &&
                     cpass_tile_lds(d->PT, R, nks, NP, false) <= 160 * 1024;
   if (tile ? cpass_tile_lds(d->PT, R, nks, NP, true) > 160 * 1024
@@ -3025,10 +3051,11 @@ static bool fin_fits(const void* kp, unsigned threads, size_t shm, int nvb) {
 QSC_API int qsc_scpass_fin_supported(const qsc_obs_desc* d, int32_t R) {
   if (!qsc_scpass_supported(d, R)) return 0;
   const int nvb = R * d->nks + 2;
-  // the C-finish work items run on 16-wave workgroups, one item per late arrival; the late
-  // arrivals must be co-resident (at least one 16-wave workgroup per CU; the launch itself
-  // checks the kernel instance's exact occupancy)
-  return (scpass_threads(d, R) == (unsigned)kFBlock && d->ntiles >= nvb &&
+  // the C-finish work items run on the fused launch's 4..16-wave workgroups (cfinish_vb's
+  // virtual waves), one item per late arrival; the late arrivals must be co-resident (at least
+  // one workgroup per CU; the launch itself checks the kernel instance's exact occupancy).
+  // Ranks up to 8 (the instances built with the finish tail).
+  return (rp_of(R) <= 8 && scpass_threads(d, R) >= 256u && d->ntiles >= nvb &&
           nvb + kFinCuMargin <= cu_count())
              ? 1
              : 0;
@@ -3098,7 +3125,7 @@ static bool loop_fits(const void* kp, unsigned threads, size_t shm, int ntiles) 
 
 QSC_API int qsc_scpass_loop_supported(const qsc_obs_desc* d, int32_t R) {
   if (!qsc_scpass_fin_supported(d, R)) return 0;
-  return d->ntiles <= cu_count() ? 1 : 0;  // one 16-wave workgroup per CU
+  return d->ntiles <= cu_count() ? 1 : 0;  // at most one workgroup per CU
 }
 
 QSC_API int qsc_scpass_loop(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,

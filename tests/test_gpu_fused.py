@@ -531,16 +531,19 @@ def test_phase_split_fused_launch_is_bitexact():
 
 
 @pytest.mark.parametrize("n", [2, 3, 11])
-@pytest.mark.parametrize("shape", [(8, 192, 192, 256), (4, 128, 128, 64)])
+@pytest.mark.parametrize("shape", [(8, 192, 192, 256, 1024), (4, 128, 128, 64, 1024),
+                                   (4, 128, 128, 64, 256),   # 4-wave workgroups (C2 class)
+                                   (3, 96, 96, 70, 384)])    # 6 waves, two ragged k-slices
 def test_fused_finish_is_bitexact(n, shape):
     """qsc_scpass_fin (S-step + next C-pass + that C-step's finish in one launch, the finish on
     the last workgroups to arrive, include/qsc.h) gives the launch pairs' S, C, moments, costs
-    and state bit for bit, eager and hipGraph."""
+    and state bit for bit, eager and hipGraph -- also on 4- and 6-wave fused workgroups, whose
+    finish items run the 16-wave sums as virtual waves."""
     from quantized_spectrum_cartography_amd.obs import Observations
     from quantized_spectrum_cartography_amd.qmc import FreeSSolver
-    R, I, J, K = shape
+    R, I, J, K, tile = shape
     d = _random_case(57, R, I, J, K)
-    o = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=R, tile=1024)
+    o = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=R, tile=tile)
     ref = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, fin=False)
     assert ref.fuse and not ref.fin
     ref.run(n)
@@ -558,7 +561,8 @@ def test_fused_finish_is_bitexact(n, shape):
 
 
 @pytest.mark.parametrize("n", [2, 3, 9])
-@pytest.mark.parametrize("shape", [(8, 192, 192, 256), (8, 384, 384, 256)])
+@pytest.mark.parametrize("shape", [(8, 192, 192, 256, 1024), (8, 384, 384, 256, 1024),
+                                   (4, 256, 256, 64, 256)])   # C2 class: 4-wave workgroups
 def test_persistent_loop_is_bitexact(n, shape):
     """qsc_scpass_loop (the n - 1 fused bodies with their C-finish in ONE persistent launch, a
     device-wide wait on the workspace's completed-items counter between bodies, include/qsc.h)
@@ -566,9 +570,9 @@ def test_persistent_loop_is_bitexact(n, shape):
     with every counter where it should be (tickets and C-finish items of every iteration)."""
     from quantized_spectrum_cartography_amd.obs import Observations
     from quantized_spectrum_cartography_amd.qmc import FreeSSolver
-    R, I, J, K = shape
+    R, I, J, K, tile = shape
     d = _random_case(58, R, I, J, K)
-    o = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=R, tile=1024)
+    o = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=R, tile=tile)
     ref = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, fin=False, loop=False)
     ref.run(n)
     nvb = R * o.desc.nks + 2
