@@ -1976,16 +1976,53 @@ __device__ void settle_s(qsc_state* __restrict__ st, const float* __restrict__ p
       npart_c, part_nll_s, part_nsq_s, nslices, hist, hist_cap, acache
 constexpr int kFWaves = kFBlock / 64;
 
+// the C-finish tile sum of the VF virtual waves vw = wave + f NWp (f < VF) of this wave: each
+// virtual wave's column partial sums its tiles vw, vw + 16, ... in order; sixteen loads in
+// flight per lane (16 / VF tiles of each virtual wave per batch), so a 4..15-wave workgroup
+// holds no more registers for it than the 16-wave one
+template <bool DEV, int VF>
+__device__ __forceinline__ void cfin_tile_sum(float (*red)[64], const float* col,
+                                              const int64_t tstride, const int ntiles,
+                                              const int wave, const int NWp, const int lane) {
+  constexpr int NW = kFWaves, JB = 16 / VF;
+  float a[VF];
+#pragma unroll
+  for (int f = 0; f < VF; ++f) a[f] = 0.0f;
+  for (int tg = 0; tg < ntiles; tg += 16 * NW) {
+    for (int jb = 0; jb < 16; jb += JB) {
+      float v[VF][JB];
+#pragma unroll
+      for (int f = 0; f < VF; ++f) {
+        const int vw = wave + f * NWp;
+#pragma unroll
+        for (int j = 0; j < JB; ++j) {
+          const int tt = tg + vw + (jb + j) * NW;
+          v[f][j] = vw < NW ? ld_fin<DEV>(&col[(int64_t)min(tt, ntiles - 1) * tstride]) : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int f = 0; f < VF; ++f) {
+        const int vw = wave + f * NWp;
+#pragma unroll
+        for (int j = 0; j < JB; ++j)
+          if (vw < NW && tg + vw + (jb + j) * NW < ntiles) a[f] += v[f][j];
+      }
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < VF; ++f)
+    if (wave + f * NWp < NW) red[wave + f * NWp][lane] = a[f];
+}
+
 // C-finish work item vb of R*nks + 2 (cfinish_kernel: vb = the workgroup; scfin_kernel: one
 // item per late-arriving workgroup), with its LDS scratch passed in.  The sums are those of a
 // 16-wave workgroup (kFWaves partial sums per column, in wave order); a smaller workgroup (the
 // fused finish of a 4..15-wave fused launch, DEV) runs them as virtual waves vw = wave,
-// wave + NWp, ... (at most VF per physical wave), same operands in the same order.
+// wave + NWp, ... (at most 4 per physical wave, cfin_tile_sum), same operands in the same order.
 template <bool DEV = false>
 __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scalars& sc,
                                            float (*sh3)[kFWaves], QSC_CF_PARAMS) {
   constexpr int NW = kFWaves;
-  constexpr int VF = DEV ? 4 : 1;  // virtual waves per physical wave (>= 4 physical waves)
   const int NWp = DEV ? (int)(blockDim.x >> 6) : NW;
   const int Kp = nks * 64;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -2089,34 +2126,14 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
     sc.as = adam_scalars_cached((step & 1) ? a1 : a0, ad, step);
   }
   // tile sum: (virtual) wave w takes tiles w, w+16, ...; sixteen independent loads in flight
-  // per group and virtual wave, the virtual waves' groups issued together
   const float* col = slab + (int64_t)r * Kp + k;
   const int64_t tstride = (int64_t)R * Kp;
-  float a[VF];
-#pragma unroll
-  for (int f = 0; f < VF; ++f) a[f] = 0.0f;
-  for (int tg = 0; tg < ntiles; tg += 16 * NW) {
-    float v[VF][16];
-#pragma unroll
-    for (int f = 0; f < VF; ++f) {
-      const int vw = wave + f * NWp;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int tt = tg + vw + j * NW;
-        v[f][j] = vw < NW ? ld_fin<DEV>(&col[(int64_t)min(tt, ntiles - 1) * tstride]) : 0.0f;
-      }
-    }
-#pragma unroll
-    for (int f = 0; f < VF; ++f) {
-      const int vw = wave + f * NWp;
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (vw < NW && tg + vw + j * NW < ntiles) a[f] += v[f][j];
-    }
-  }
-#pragma unroll
-  for (int f = 0; f < VF; ++f)
-    if (wave + f * NWp < NW) red[wave + f * NWp][lane] = a[f];
+  if (!DEV || NWp >= NW)
+    cfin_tile_sum<DEV, 1>(red, col, tstride, ntiles, wave, NWp, lane);
+  else if (2 * NWp >= NW)
+    cfin_tile_sum<DEV, 2>(red, col, tstride, ntiles, wave, NWp, lane);
+  else
+    cfin_tile_sum<DEV, 4>(red, col, tstride, ntiles, wave, NWp, lane);
   __syncthreads();
   if (wave == 0 && k < K) {
     float g = red[0][lane];
@@ -2161,6 +2178,15 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(QSC_CF_PARAMS) {
 // holding the CUs despite the check) sets the state's sticky fault word and skips the item.
 constexpr unsigned kFinSpin = 1u << 20;
 
+// One poll of a cross-workgroup counter (arrival tickets, completed C-finish items): a relaxed
+// agent-scope load (`global_load ... sc1`).  Polling with an atomic add of an opaque zero
+// instead (a literal zero is folded back into the load) was measured: no change for the fused
+// finish, 23.6 -> 33.5 us per persistent-loop iteration at C3 (256 workgroups polling one
+// line with atomics).
+__device__ __forceinline__ unsigned long long poll_ctr(unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int RP, typename E, int KIND, bool LOG>
 __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
     QSC_SCFIN_KPARAMS, float* __restrict__ mC, float* __restrict__ vC, qsc_adam adc,
@@ -2202,7 +2228,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
     if (vb >= 0) {
       const unsigned long long target = tk - a + (unsigned long long)nt;
       unsigned polls = 0;
-      while (__hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      while (poll_ctr(ticket) < target) {
         if (++polls > kFinSpin) {
           __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           vb = -1;
@@ -2324,7 +2350,7 @@ __device__ __forceinline__ bool scloop_iter(LoopKA* kb, const int t, const unsig
     if (vb >= 0) {
       const unsigned long long target = tk - a + (unsigned long long)nt;
       unsigned polls = 0;
-      while (__hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      while (poll_ctr(ticket) < target) {
         if (++polls > kFinSpin) {
           __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           vb = kLoopTimeout;
@@ -2359,7 +2385,7 @@ __device__ __forceinline__ bool scloop_iter(LoopKA* kb, const int t, const unsig
     const unsigned long long target = done0 + (unsigned long long)nvb * (unsigned long long)(it + 1);
     unsigned polls = 0;
     int ok = 1;
-    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    while (poll_ctr(done) < target) {
       if (++polls > kFinSpin) {
         __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
