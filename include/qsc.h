@@ -460,9 +460,10 @@ QSC_API int qsc_cpass_nsq(const qsc_obs_desc* d, const void* c_entries, const in
 /* byte offset, in the pass workspace, of the float where qsc_cpass / qsc_cpass_nsq leave ||C||^2
  * of the C they read (the fixed order of qsc_sumsq_small): a K-slab solver all-reduces it in
  * place and hands it to qsc_cfinish as normsq_c_ext.  -1 on an invalid descriptor. */
-/* byte offset in the pass workspace of the fused-finish launches' counters (two uint64 on
- * 128-B lines of their own: arrival tickets, then the persistent loop's completed C-finish
- * items), for diagnostics; the workspace must be zero-filled before its first use */
+/* byte offset in the pass workspace of the fused-finish launches' counters, for diagnostics:
+ * uint64 words each on a 128-B line of its own -- word 16 g (g < 8): the arrival tickets of tile
+ * group g (tiles t with t mod 8 == g), word 128: completed groups, word 144: the persistent
+ * loop's completed C-finish items.  The workspace must be zero-filled before its first use. */
 QSC_API int64_t qsc_pass_sync_offset(const qsc_obs_desc* d, int32_t R);
 QSC_API int64_t qsc_pass_cnsq_offset(const qsc_obs_desc* d, int32_t R);
 /* ||x||^2 into *out (fp32, fixed order), e.g. the local ||C_slab||^2 before an all-reduce */

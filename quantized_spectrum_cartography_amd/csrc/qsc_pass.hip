@@ -2163,20 +2163,21 @@ __global__ void __launch_bounds__(kFBlock) cfinish_kernel(QSC_CF_PARAMS) {
 // ---------------------------------------------------------------------------------------
 // Fused launch with the C-finish at its tail (qsc_scpass_fin)
 // ---------------------------------------------------------------------------------------
-// scfused_tile, then each workgroup takes an arrival ticket (device-scope atomic on the state's
-// fin_ticket word, after its writes are made visible device-wide); the LAST R*nks + 2 arrivals
-// wait until every tile has arrived and then run the C-finish work items (cfinish_vb), the
-// earlier ones leave.  The C-step finish that was a launch of its own rides on the tail of the
-// fused launch: same code, operands and order as (qsc_scpass, qsc_cfinish mode 1), so the same
-// results bit for bit, one launch per iteration instead of two.  Co-residency: a waiting
-// workgroup keeps its CU, and it is one of the last R*nks + 2 to arrive, so the waiters plus
-// the tiles still to arrive are at most R*nks + 2 workgroups that must be resident together;
-// the host checks that against the kernel's occupancy times the CU count, with a margin for
-// other streams (qsc_scpass_fin_supported, fin_fits), the workgroups that already left free
-// their CUs for the rest.  Tickets count up for the life of the state (it is zeroed with it);
-// launch j's arrivals hold tickets [j*nt, (j+1)*nt).  A wait past kFinSpin polls (other work
-// holding the CUs despite the check) sets the state's sticky fault word and skips the item.
+// scfused_tile, then each workgroup takes an arrival ticket (device-scope atomic on its tile
+// group's workspace counter, after its writes are complete device-wide, fin_arrive); the last
+// arrivals of each group, R*nks + 2 workgroups in all, wait until every tile has arrived and
+// then run the C-finish work items (cfinish_vb), the others leave.  The C-step finish that was
+// a launch of its own rides on the tail of the fused launch: same code, operands and order as
+// (qsc_scpass, qsc_cfinish mode 1), so the same results bit for bit, one launch per iteration
+// instead of two.  Co-residency: a waiting workgroup keeps its CU; at most R*nks + 2 wait, so
+// every other tile finds a CU as long as the device holds more workgroups than that -- the host
+// checks it against the kernel's occupancy times the CU count, with a margin for other streams
+// (qsc_scpass_fin_supported, fin_fits).  A wait past kFinSpin polls (other work holding the CUs
+// despite the check) sets the state's sticky fault word and skips the item.
 constexpr unsigned kFinSpin = 1u << 20;
+constexpr int kFinGroups = 8;                      // arrival-ticket groups (PassWs::sync)
+constexpr int kSyncDone = 16 * (kFinGroups + 1);   // PassWs::sync word: completed C-finish items
+constexpr int kSyncWords = 16 * (kFinGroups + 2);
 
 // One poll of a cross-workgroup counter (arrival tickets, completed C-finish items): a relaxed
 // agent-scope load (`global_load ... sc1`).  Polling with an atomic add of an opaque zero
@@ -2185,6 +2186,39 @@ constexpr unsigned kFinSpin = 1u << 20;
 // line with atomics).
 __device__ __forceinline__ unsigned long long poll_ctr(unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Arrival of tile t at the fused finish (thread 0 of its workgroup, after its stores completed):
+// the tiles count in kFinGroups groups (t mod G) on counters of their own -- the atomics on one
+// counter are serialised, and at C2 the tiles of a launch arrive together (measured: tools/micro/
+// atomic_contention.hip) -- and the last arrival of a group counts the group complete.  The last
+// q_g arrivals of group g run the C-finish items g, g + G, ... (q_g of them; all R*nks + 2 over
+// the groups) once every group is complete.  Counters run for the life of the workspace: every
+// launch adds n_g to group g and G to the completed count (the same tile count every launch).
+// Returns the item (-1: none) or `timeout_vb` when the wait passed kFinSpin polls.
+__device__ __forceinline__ int fin_arrive(unsigned long long* sync, const int t, const int nt,
+                                          const int nvb, int* fault, const int timeout_vb) {
+  const int G = nt < kFinGroups ? nt : kFinGroups;
+  const int g = t % G;
+  const unsigned long long ng = (unsigned long long)((nt - g + G - 1) / G);
+  const unsigned long long qg = g < nvb ? (unsigned long long)((nvb - g + G - 1) / G) : 0ull;
+  const unsigned long long tk =
+      __hip_atomic_fetch_add(sync + 16 * g, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long a = tk % ng, launch = tk / ng;
+  unsigned long long* const groups = sync + 16 * kFinGroups;
+  if (a == ng - 1) __hip_atomic_fetch_add(groups, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a + qg < ng) return -1;
+  const int vb = g + G * (int)(a + qg - ng);
+  const unsigned long long target = (launch + 1) * (unsigned long long)G;
+  unsigned polls = 0;
+  while (poll_ctr(groups) < target) {
+    if (++polls > kFinSpin) {
+      __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return timeout_vb;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return vb;
 }
 
 template <int RP, typename E, int KIND, bool LOG>
@@ -2201,46 +2235,26 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
   float(*sh3)[kFWaves] = reinterpret_cast<float(*)[kFWaves]>(smem + kFWaves * 64);
   Scalars& sc = *reinterpret_cast<Scalars*>(smem + kFWaves * 64 + 3 * kFWaves);
   int* vbl = reinterpret_cast<int*>(smem + kFWaves * 64 + 3 * kFWaves + 16);
-  // the arrival ticket (PassWs::sync[0]; 64-bit: it counts every workgroup of every launch for
-  // the life of the workspace, and must stay aligned to launches, so it may never wrap)
-  unsigned long long* ticket = sync;
   int* fault = reinterpret_cast<int*>(st) + 9;              // qsc_state.fused_fault
   // Ordering, chosen for the 8 non-coherent XCD L2s: everything the C-finish items read was
   // stored write-through at agent scope by the tile body (st_fin), so each wave waits for its
   // own stores to complete (vmcnt 0: at the device coherence point), the workgroup barrier
-  // joins the waves, and thread 0 takes its ticket with a relaxed agent-scope increment -- no
-  // release fence, whose L2 write-back per workgroup (while 25 MB of S-step writes stream
-  // through the L2s) cost ~6 us per launch.  Waiters poll with relaxed agent-scope loads
-  // (L2-bypassing, no invalidate: an acquire load per poll would invalidate this XCD's L2 under
-  // the workgroups still running there, measured 160 us per launch instead of ~34) and take
-  // one acquire fence after the wait (the state line may sit stale in this XCD's L2).
+  // joins the waves, and thread 0 takes its arrival ticket with a relaxed agent-scope increment
+  // (fin_arrive; 64-bit counters: they count every workgroup of every launch for the life of the
+  // workspace and must stay aligned to launches, so they may never wrap) -- no release fence,
+  // whose L2 write-back per workgroup (while 25 MB of S-step writes stream through the L2s) cost
+  // ~6 us per launch.  Waiters poll with relaxed agent-scope loads (an acquire load per poll
+  // would invalidate this XCD's L2 under the workgroups still running there, measured 160 us per
+  // launch instead of ~34) and take no acquire fence: every value the C-finish item reads from
+  // this launch's other workgroups is loaded sc1 (ld_fin); C, mC, vC and the C-side Adam cache
+  // are from the previous launch.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned long long tk =
-        __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long a = tk % (unsigned long long)nt;
-    int vb = (int)a - (nt - nvb);
 #if QSC_DIAG_STAMPS
     g_stamps[(int)blockIdx.x * (FusedBlock<RP>::v / 64) * kStamps + 19] = __builtin_amdgcn_s_memtime();
-    g_stamps[(int)blockIdx.x * (FusedBlock<RP>::v / 64) * kStamps + 18] = (unsigned long long)a;
 #endif
-    if (vb >= 0) {
-      const unsigned long long target = tk - a + (unsigned long long)nt;
-      unsigned polls = 0;
-      while (poll_ctr(ticket) < target) {
-        if (++polls > kFinSpin) {
-          __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          vb = -1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      // (no acquire fence: every value the C-finish item reads from this launch's other
-      // workgroups is loaded sc1, ld_fin; C, mC, vC and the C-side Adam cache are from the
-      // previous launch)
-    }
-    *vbl = vb;
+    *vbl = fin_arrive(sync, (int)blockIdx.x, nt, nvb, fault, -1);
   }
   [[maybe_unused]] const int wg = (int)blockIdx.x * (FusedBlock<RP>::v / 64) + (threadIdx.x >> 6);
   STAMP(wg, 20);  // (diagnostic builds) wave 0: ticket taken and, for a waiter, the wait over
@@ -2301,7 +2315,7 @@ struct LoopArgs {
   float lambda_s, lambda_c;
   int nks, NP, PT, nbins, R, K, hist_cap, n;
   int* progress;  // nullable diagnostics: per workgroup, 16 * iteration + phase reached
-  unsigned long long* sync;  // PassWs::sync: [0] tickets, [16] completed C-finish items
+  unsigned long long* sync;  // PassWs::sync: group tickets, completed groups and C-finish items
   Edges E;
 };
 using LoopKA = const char __attribute__((address_space(4)));
@@ -2335,31 +2349,15 @@ __device__ __forceinline__ bool scloop_iter(LoopKA* kb, const int t, const unsig
   Scalars& sc = *reinterpret_cast<Scalars*>(smem + kFWaves * 64 + 3 * kFWaves);
   int* vbl = reinterpret_cast<int*>(smem + kFWaves * 64 + 3 * kFWaves + 16);
   unsigned long long* const sync = QSC_LA(sync);
-  unsigned long long* ticket = sync;
-  unsigned long long* done = sync + 16;
+  unsigned long long* done = sync + kSyncDone;
   int* fault = reinterpret_cast<int*>(st) + 9;
   mark(2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (st_fin stores complete: see scfin)
   __syncthreads();
   if (tidx == 0) {
-    const unsigned long long tk =
-        __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long a = tk % (unsigned long long)nt;
-    int vb = (int)a - (nt - nvb);  // >= 0: a C-finish item; -1: none; kLoopTimeout: timed out
-    if (vb < 0) vb = -1;
-    if (vb >= 0) {
-      const unsigned long long target = tk - a + (unsigned long long)nt;
-      unsigned polls = 0;
-      while (poll_ctr(ticket) < target) {
-        if (++polls > kFinSpin) {
-          __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          vb = kLoopTimeout;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      if (vb >= 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
+    // >= 0: a C-finish item; -1: none; kLoopTimeout: timed out
+    const int vb = fin_arrive(sync, t, nt, nvb, fault, kLoopTimeout);
+    if (vb >= 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     *vbl = vb;
   }
   __syncthreads();
@@ -2414,7 +2412,7 @@ __global__ void __launch_bounds__(FusedBlock<RP>::v) scloop_kernel(LoopArgs args
     // the fin_done base: every finish of this launch completes after every workgroup has taken
     // its first ticket, i.e. after this read (thread 0 keeps it)
     if (threadIdx.x == 0)
-      done0 = __hip_atomic_load(QSC_LA(sync) + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      done0 = __hip_atomic_load(QSC_LA(sync) + kSyncDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   (void)args;
   for (int it = 0; it < n; ++it) {
@@ -2615,7 +2613,8 @@ struct PassWs {
   float* cnsq;      // ||C||^2 of the C the last C-pass read (written by the C-pass)
   AdamCache* acache;  // [0..1] S-side, [2..3] C-side step scalars (adam_scalars_cached)
   // cross-workgroup counters of the fused-finish launches, each on a 128-B line of its own that
-  // only atomics and agent-scope (sc1) loads touch: [0] arrival tickets, [16] the persistent
+  // only atomics and agent-scope (sc1) loads touch: [16 g] the arrival tickets of tile group g
+  // (g < kFinGroups), [16 kFinGroups] completed groups, [16 (kFinGroups + 1)] the persistent
   // loop's completed C-finish items.  An sc1 load is served by the XCD's L2, so a counter on a
   // line that plain loads also bring into an L2 (the state's other fields) can be read stale
   // there for as long as the line stays (seen: a persistent-loop wait that never ended).
@@ -2653,7 +2652,7 @@ size_t ws_bytes_for(const qsc_obs_desc* d, int R) {
   const int64_t Kp = (int64_t)d->nks * 64;
   return al((size_t)d->ntiles * R * Kp * 4) + al((size_t)d->ntiles * d->nks * 4) +
          2 * al((size_t)(d->Pp / QSC_SLICE) * 4) + al(256 * 8) + al((kSchedQ + 1) * 4) + al(4) +
-         al(4 * sizeof(AdamCache)) + al(32 * sizeof(unsigned long long));
+         al(4 * sizeof(AdamCache)) + al(kSyncWords * sizeof(unsigned long long));
 }
 
 bool desc_ok(const qsc_obs_desc* d) {

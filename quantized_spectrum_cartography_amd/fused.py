@@ -127,8 +127,9 @@ class PassEngine:
         off = int(_lib.lib().qsc_pass_sync_offset(self.desc, self.R))
         if off < 0:
             raise _lib.QscError("qsc_pass_sync_offset failed")
-        raw = self.ws[off:off + 256].cpu()
-        return int(raw[0:8].view(torch.int64).item()), int(raw[128:136].view(torch.int64).item())
+        # uint64 words (include/qsc.h): 16 g group tickets (g < 8), 128 groups, 144 items
+        w = self.ws[off:off + 160 * 8].cpu().view(torch.int64)
+        return int(w[0:128:16].sum().item()), int(w[144].item())
 
     def scpass_loop_supported(self):
         return bool(_lib.lib().qsc_scpass_loop_supported(self.desc, self.R))

@@ -60,25 +60,48 @@ def test_every_package_module_imports():
         importlib.import_module("%s.%s" % (pkg.__name__, m.name))
 
 
-def _fin_roles(tickets, nt, nvb):
-    """The fused-finish arrival protocol of scfin_kernel (csrc/qsc_pass.hip), restated: a
-    workgroup holding ticket tk (64-bit, never wraps) is arrival a = tk mod nt of its launch; the
-    last nvb arrivals run C-finish item a - (nt - nvb) once the counter reaches tk - a + nt."""
-    return [(tk % nt - (nt - nvb), tk - tk % nt + nt) for tk in tickets]
+def _fin_arrive(ctr, t, nt, nvb, G_max=8):
+    """The fused-finish arrival protocol of fin_arrive (csrc/qsc_pass.hip), restated: tile t
+    counts on its group's counter (group g = t mod G, G = min(8, nt), n_g tiles); the group's
+    last arrival counts the group complete; the last q_g arrivals of group g run C-finish items
+    g, g + G, ... once the completed-group count reaches (launch + 1) G.  Counters are 64-bit and
+    count for the life of the workspace.  Returns (item or -1, wait target or None)."""
+    G = min(G_max, nt)
+    g = t % G
+    ng = (nt - g + G - 1) // G
+    qg = (nvb - g + G - 1) // G if g < nvb else 0
+    tk = ctr[g]
+    ctr[g] += 1
+    a, launch = tk % ng, tk // ng
+    if a == ng - 1:
+        ctr["groups"] += 1
+    if a + qg < ng:
+        return -1, None
+    return g + G * (a + qg - ng), (launch + 1) * G
 
 
 def test_fused_finish_ticket_protocol():
-    """Every launch's last R*nks + 2 arrivals take each C-finish item exactly once, all of them
-    wait for the same count -- the launch's last ticket + 1 -- and the earlier arrivals leave;
-    over consecutive launches of any tile count (tickets count up for the life of the state)."""
-    for nt, nvb in ((256, 34), (64, 6), (34, 34), (36, 34), (1000, 130)):
+    """Every launch's C-finish items are each taken exactly once, by workgroups that wait for the
+    same completed-group count, which is reached exactly when the launch's last tile arrives;
+    any arrival order, any tile count >= R*nks + 2, consecutive launches (counters count up for
+    the life of the workspace, from any start)."""
+    import random
+    rng = random.Random(5)
+    for nt, nvb in ((256, 34), (64, 6), (34, 34), (36, 34), (1000, 130), (5, 3), (512, 6)):
+        G = min(8, nt)
         for start_launch in (0, 7, 10 ** 12):
+            ctr = {g: start_launch * ((nt - g + G - 1) // G) for g in range(G)}
+            ctr["groups"] = start_launch * G
             for launch in range(3):
-                first = (start_launch + launch) * nt
-                tickets = [first + i for i in range(nt)]  # in arrival order
-                roles = _fin_roles(tickets, nt, nvb)
+                order = list(range(nt))
+                rng.shuffle(order)
+                roles, done_at = [], None
+                for i, t in enumerate(order):
+                    roles.append(_fin_arrive(ctr, t, nt, nvb))
+                    if done_at is None and ctr["groups"] >= (start_launch + launch + 1) * G:
+                        done_at = i
                 assert sorted(vb for vb, _ in roles if vb >= 0) == list(range(nvb))
-                assert [vb >= 0 for vb, _ in roles] == [i >= nt - nvb for i in range(nt)]
-                assert {t for vb, t in roles if vb >= 0} == {first + nt}
-                # the wait (counter >= target) ends exactly when the launch's last ticket is taken
-                assert [first + i >= first + nt for i in range(nt + 1)] == [False] * nt + [True]
+                assert {w for vb, w in roles if vb >= 0} == {(start_launch + launch + 1) * G}
+                # the waiters' count is reached exactly at the launch's last arrival
+                assert done_at == nt - 1
+                assert ctr["groups"] == (start_launch + launch + 1) * G

@@ -4,6 +4,10 @@
 # C3.  OUT=gpurun_out/t24 bash tools/gpu_r04c.sh
 OUT=${OUT:-gpurun_out/r04c}
 mkdir -p $OUT
+if [ -x tools/micro/atomic_contention ]; then
+  timeout -k 5 60 ./tools/micro/atomic_contention > $OUT/atomic_contention.log 2>&1 || { cat $OUT/atomic_contention.log; exit 1; }
+  cat $OUT/atomic_contention.log
+fi
 echo "# HEAD $(cat .head_sha)" > $OUT/pytest_fin_loop.log
 timeout -k 10 300 python -u -m pytest tests/test_gpu_fused.py -x -q --timeout 120 \
   --timeout-method thread -k "fused_finish or persistent_loop" >> $OUT/pytest_fin_loop.log 2>&1 \
