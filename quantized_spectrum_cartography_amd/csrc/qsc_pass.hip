@@ -1984,29 +1984,36 @@ template <bool DEV, int VF>
 __device__ __forceinline__ void cfin_tile_sum(float (*red)[64], const float* col,
                                               const int64_t tstride, const int ntiles,
                                               const int wave, const int NWp, const int lane) {
-  constexpr int NW = kFWaves, JB = 16 / VF;
+  // NGB: groups of 16 NW tiles per batch -- two in the standalone C-finish (32 loads in
+  // flight: C2's 512 tiles in one round trip), one in the fused finish (its tile body's registers)
+  constexpr int NW = kFWaves, JB = 16 / VF, NGB = DEV ? 1 : 2;
   float a[VF];
 #pragma unroll
   for (int f = 0; f < VF; ++f) a[f] = 0.0f;
-  for (int tg = 0; tg < ntiles; tg += 16 * NW) {
+  for (int tg = 0; tg < ntiles; tg += NGB * 16 * NW) {
     for (int jb = 0; jb < 16; jb += JB) {
-      float v[VF][JB];
+      float v[NGB][VF][JB];
 #pragma unroll
-      for (int f = 0; f < VF; ++f) {
-        const int vw = wave + f * NWp;
+      for (int gb = 0; gb < NGB; ++gb)
 #pragma unroll
-        for (int j = 0; j < JB; ++j) {
-          const int tt = tg + vw + (jb + j) * NW;
-          v[f][j] = vw < NW ? ld_fin<DEV>(&col[(int64_t)min(tt, ntiles - 1) * tstride]) : 0.0f;
+        for (int f = 0; f < VF; ++f) {
+          const int vw = wave + f * NWp;
+#pragma unroll
+          for (int j = 0; j < JB; ++j) {
+            const int tt = tg + gb * 16 * NW + vw + (jb + j) * NW;
+            v[gb][f][j] =
+                vw < NW ? ld_fin<DEV>(&col[(int64_t)min(tt, ntiles - 1) * tstride]) : 0.0f;
+          }
         }
-      }
 #pragma unroll
-      for (int f = 0; f < VF; ++f) {
-        const int vw = wave + f * NWp;
+      for (int gb = 0; gb < NGB; ++gb)
 #pragma unroll
-        for (int j = 0; j < JB; ++j)
-          if (vw < NW && tg + vw + (jb + j) * NW < ntiles) a[f] += v[f][j];
-      }
+        for (int f = 0; f < VF; ++f) {
+          const int vw = wave + f * NWp;
+#pragma unroll
+          for (int j = 0; j < JB; ++j)
+            if (vw < NW && tg + gb * 16 * NW + vw + (jb + j) * NW < ntiles) a[f] += v[gb][f][j];
+        }
     }
   }
 #pragma unroll
