@@ -21,17 +21,21 @@ def ctypes_copy(dst, src):
 
 
 def default_tile(P, R, K):
-    """C-pass pixel tile (positions, a power of two in [128, 1024]).
+    """C-pass pixel tile (positions, a power of two in [256, 1024]; 128 at rank 16 when LDS
+    requires it).
 
     The C-pass runs one 4-wave workgroup per (tile, 64-bin slice): aim for ~1024 workgroups
     (4 per CU) while keeping tiles large, since the per-bin lists of a tile are padded to their
-    longest (bigger tiles -> relatively less padding) and the tile's S rows live in LDS."""
+    longest (bigger tiles -> relatively less padding) and the tile's S rows live in LDS.  At
+    least 256 positions: the fused launch (one workgroup per tile) then runs two S-step slices
+    per wave and its C-finish sums half as many tiles -- C2 (256^2 x 64) 131.4 k grad-steps/s
+    at 256 against 129.8 k at 128 (profiles/r04/fin_small_wg/ab_c2*.log)."""
     if os.environ.get("QSC_CTILE"):  # tuning override (power of two, 64..4096)
         return int(os.environ["QSC_CTILE"])
     Pp = -(-P // 64) * 64
     nks = -(-K // 64)
     want = max(1, (Pp * nks) // 1024)
-    t = 128
+    t = 256
     while t * 2 <= want and t < 1024:
         t *= 2
     if R > 8:
