@@ -1984,9 +1984,9 @@ template <bool DEV, int VF>
 __device__ __forceinline__ void cfin_tile_sum(float (*red)[64], const float* col,
                                               const int64_t tstride, const int ntiles,
                                               const int wave, const int NWp, const int lane) {
-  // NGB: groups of 16 NW tiles per batch -- two in the standalone C-finish (32 loads in
-  // flight: C2's 512 tiles in one round trip), one in the fused finish (its tile body's registers)
-  constexpr int NW = kFWaves, JB = 16 / VF, NGB = DEV ? 1 : 2;
+  // NGB: groups of 16 NW tiles per batch.  Two in the standalone C-finish (32 loads in flight)
+  // made it slower, 3.26 -> 4.6 us at C3 (profiles/r04/fin_small_wg/ab_c3_grouped_tickets.log)
+  constexpr int NW = kFWaves, JB = 16 / VF, NGB = 1;
   float a[VF];
 #pragma unroll
   for (int f = 0; f < VF; ++f) a[f] = 0.0f;
