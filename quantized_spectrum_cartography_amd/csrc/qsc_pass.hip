@@ -39,9 +39,11 @@ constexpr int kSWaves = kSBlock / 64;
 #endif
 constexpr int kCBlock = QSC_CPASS_BLOCK;  // C-pass: kCBlock/64 waves = parts of one (tile, 64-bin slice)
 // C-pass tile form: a bin list is split into parts while each part keeps at least this many
-// 4-entry chunks (every C-pass form and the fused launches share the partition)
+// 4-entry chunks and the tile form's LDS (at the signed-row size, so that both row formats of a
+// layout get the same partition) fits (tile_parts; every C-pass form and the fused launches
+// share the partition).  C2: 1.5 against 3.0, 145 k -> 148 k grad-steps/s
 #ifndef QSC_CPART_MIN_CHUNKS
-#define QSC_CPART_MIN_CHUNKS 3.0
+#define QSC_CPART_MIN_CHUNKS 1.5
 #endif
 constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 
@@ -1440,6 +1442,27 @@ size_t cpass_tile_lds(int PT, int R, int nks, int NP, bool sr) {
   const size_t U = (size_t)nks * NP;
   return tfloats(PT, R, sr) * 4 + 2 * 256 * 4 + (NP > 1 ? U * R * 64 * 4 : 0) +
          std::max<size_t>(U, 16) * 4;
+}
+
+#ifndef QSC_CPASS_TILE
+#define QSC_CPASS_TILE 1
+#endif
+#ifndef QSC_CTILE_MAXW
+#define QSC_CTILE_MAXW 16
+#endif
+// The C-pass tile partition of a layout: NP parts per bin list, up to 16 waves per tile, while
+// a part keeps >= QSC_CPART_MIN_CHUNKS 4-entry chunks and the tile form's LDS fits at the
+// signed-row size (the same NP for both row formats); true when the tile form applies (>= 4
+// units, LDS fits at the layout's own row format `sr`)
+static bool tile_parts(const qsc_obs_desc* d, int R, bool sr, int* np) {
+  const int nks = d->nks;
+  int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
+  const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
+  while (NP > 1 && (chunks / NP < QSC_CPART_MIN_CHUNKS ||
+                    cpass_tile_lds(d->PT, R, nks, NP, true) > 160 * 1024))
+    --NP;
+  *np = NP;
+  return QSC_CPASS_TILE && nks * NP >= 4 && cpass_tile_lds(d->PT, R, nks, NP, sr) <= 160 * 1024;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2890,21 +2913,14 @@ static int cpass_impl(const qsc_obs_desc* d, const void* c_entries, const int32_
   else if (!m->log_model)
     scale_edges(&E, m->nbounds - 1, lk.a);
   hipStream_t s = STREAM(stream);
-#ifndef QSC_CPASS_TILE
-#define QSC_CPASS_TILE 1
-#endif
   if (QSC_CPASS_TILE) {
-    // tile form: up to 16 waves per tile; parts per bin list while a part keeps >= 3 chunks
-#ifndef QSC_CTILE_MAXW
-#define QSC_CTILE_MAXW 16
-#endif
+    // tile form: up to 16 waves per tile, the partition of tile_parts
     const int nks = d->nks;
-    int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
-    const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
-    while (NP > 1 && chunks / NP < QSC_CPART_MIN_CHUNKS) --NP;
+    int NP = 1;
+    const bool tile = tile_parts(d, R, sr, &NP);
     const int U = nks * NP;
     const size_t tshm = cpass_tile_lds(d->PT, R, nks, NP, sr);
-    if (U >= 4 && tshm <= 160 * 1024) {
+    if (tile) {
       const dim3 tb((unsigned)(64 * std::min(U, QSC_CTILE_MAXW)));
 #define CPASS_TILE_LAUNCH(RPV, ET, KD, LG)                                                     \
   hipLaunchKernelGGL((cpass_tile_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles), tb, tshm, \
@@ -2934,13 +2950,8 @@ static int cpass_impl(const qsc_obs_desc* d, const void* c_entries, const int32_
 // uses for this layout -- the tile form's NP, or kCParts where qsc_cpass falls back to the
 // per-(tile, k-slice) form -- so that the fused launch sums every dC in the same order
 static int cpass_parts(const qsc_obs_desc* d, int R, bool sr) {
-  const int nks = d->nks;
-  int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
-  const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
-  while (NP > 1 && chunks / NP < QSC_CPART_MIN_CHUNKS) --NP;
-  const bool tile = QSC_CPASS_TILE && nks * NP >= 4 &&
-                    cpass_tile_lds(d->PT, R, nks, NP, sr) <= 160 * 1024;
-  return tile ? NP : kCParts;
+  int NP = 1;
+  return tile_parts(d, R, sr, &NP) ? NP : kCParts;
 }
 
 // the fused launch applies (its C-pass partition and LDS fit), with or without signed rows
@@ -2963,15 +2974,9 @@ static bool sr_layout_ok(const qsc_obs_desc* d, int R) {
     return false;
   const int RP = rp_of(R);
   if (spass_lds(d, R, true) * spass_bpc(RP) > 160 * 1024) return false;
-  const int nks = d->nks;
-  int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
-  const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
-  while (NP > 1 && chunks / NP < QSC_CPART_MIN_CHUNKS) --NP;
-  const bool tile = QSC_CPASS_TILE && nks * NP >= 4 &&
-                    cpass_tile_lds(d->PT, R, nks, NP, false) <= 160 * 1024;
-  if (tile ? cpass_tile_lds(d->PT, R, nks, NP, true) > 160 * 1024
-           : cpass_lds(d, R, true) > 160 * 1024)
-    return false;
+  int np0 = 1, np1 = 1;
+  const bool tile = tile_parts(d, R, false, &np0);
+  if (tile ? !tile_parts(d, R, true, &np1) : cpass_lds(d, R, true) > 160 * 1024) return false;
   if (scpass_fits(d, R, false) && !scpass_fits(d, R, true)) return false;
   return true;
 }
@@ -2992,10 +2997,15 @@ QSC_API int qsc_scpass_supported(const qsc_obs_desc* d, int32_t R) {
   return scpass_fits(d, R, d->rowfmt == 1) ? 1 : 0;
 }
 
-// threads of the fused launch at rank R (waves: two S-step slices each, 4..16; 4..8 at rank 16)
+// threads of the fused launch at rank R (waves: two S-step slices each, 4..16; 4..8 at rank 16;
+// one slice each on tiles of at most QSC_FUSED_ONE_SLICE slices)
+#ifndef QSC_FUSED_ONE_SLICE
+#define QSC_FUSED_ONE_SLICE 16  // C2 (8-slice tiles, 8 waves): 133 k -> 145 k grad-steps/s
+#endif
 static unsigned scpass_threads(const qsc_obs_desc* d, int R) {
   const int nsl = d->PT / QSC_SLICE;
-  return 64u * (unsigned)std::min(rp_of(R) > 8 ? 8 : QSC_FUSED_WAVES, std::max(4, nsl / 2));
+  const int per = nsl <= QSC_FUSED_ONE_SLICE ? nsl : nsl / 2;
+  return 64u * (unsigned)std::min(rp_of(R) > 8 ? 8 : QSC_FUSED_WAVES, std::max(4, per));
 }
 
 QSC_API int32_t qsc_scpass_split_rows(const qsc_obs_desc* d, int32_t R) {
