@@ -532,12 +532,13 @@ def test_phase_split_fused_launch_is_bitexact():
 
 @pytest.mark.parametrize("n", [2, 3, 11])
 @pytest.mark.parametrize("shape", [(8, 192, 192, 256, 1024), (4, 128, 128, 64, 1024),
-                                   (4, 128, 128, 64, 256),   # 4-wave workgroups (C2 class)
-                                   (3, 96, 96, 70, 384)])    # 6 waves, two ragged k-slices
+                                   (4, 128, 128, 64, 128),   # 4-wave workgroups
+                                   (4, 128, 128, 64, 256),   # 8 waves (C2 class)
+                                   (3, 96, 96, 70, 384)])    # 12 waves, two ragged k-slices
 def test_fused_finish_is_bitexact(n, shape):
     """qsc_scpass_fin (S-step + next C-pass + that C-step's finish in one launch, the finish on
     the last workgroups to arrive, include/qsc.h) gives the launch pairs' S, C, moments, costs
-    and state bit for bit, eager and hipGraph -- also on 4- and 6-wave fused workgroups, whose
+    and state bit for bit, eager and hipGraph -- also on 4..15-wave fused workgroups, whose
     finish items run the 16-wave sums as virtual waves."""
     from quantized_spectrum_cartography_amd.obs import Observations
     from quantized_spectrum_cartography_amd.qmc import FreeSSolver
@@ -562,7 +563,7 @@ def test_fused_finish_is_bitexact(n, shape):
 
 @pytest.mark.parametrize("n", [2, 3, 9])
 @pytest.mark.parametrize("shape", [(8, 192, 192, 256, 1024), (8, 384, 384, 256, 1024),
-                                   (4, 256, 256, 64, 256)])   # C2 class: 4-wave workgroups
+                                   (4, 256, 256, 64, 256)])   # C2 class: 8-wave workgroups
 def test_persistent_loop_is_bitexact(n, shape):
     """qsc_scpass_loop (the n - 1 fused bodies with their C-finish in ONE persistent launch, a
     device-wide wait on the workspace's completed-items counter between bodies, include/qsc.h)
