@@ -1450,20 +1450,6 @@ size_t cpass_tile_lds(int PT, int R, int nks, int NP, bool sr) {
 #ifndef QSC_CTILE_MAXW
 #define QSC_CTILE_MAXW 16
 #endif
-// The C-pass tile partition of a layout: NP parts per bin list, up to 16 waves per tile, while
-// a part keeps >= QSC_CPART_MIN_CHUNKS 4-entry chunks and the tile form's LDS fits at the
-// signed-row size (the same NP for both row formats); true when the tile form applies (>= 4
-// units, LDS fits at the layout's own row format `sr`)
-static bool tile_parts(const qsc_obs_desc* d, int R, bool sr, int* np) {
-  const int nks = d->nks;
-  int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
-  const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
-  while (NP > 1 && (chunks / NP < QSC_CPART_MIN_CHUNKS ||
-                    cpass_tile_lds(d->PT, R, nks, NP, true) > 160 * 1024))
-    --NP;
-  *np = NP;
-  return QSC_CPASS_TILE && nks * NP >= 4 && cpass_tile_lds(d->PT, R, nks, NP, sr) <= 160 * 1024;
-}
 
 // ---------------------------------------------------------------------------------------
 // Fused S-step + next C-pass, one workgroup per C-pass pixel tile (16 waves; 8 at rank 16).
@@ -1949,6 +1935,24 @@ size_t scfused_lds(int PT, int R, int K, int nks, int NP, bool sr) {
   const size_t U = (size_t)nks * NP;
   return 32 + tfloats(K, R, sr) * 4 + 256 * 8 + tfloats(PT, R, sr) * 4 +
          (NP > 1 ? U * R * 64 * 4 : 0) + std::max<size_t>(U, 16) * 4;
+}
+
+// The C-pass tile partition of a layout: NP parts per bin list, up to 16 waves per tile, while
+// a part keeps >= QSC_CPART_MIN_CHUNKS 4-entry chunks and, at the signed-row size (the same NP
+// for both row formats), the tile form's LDS fits and so does the fused launch's where it can
+// fit at all; true when the tile form applies (>= 4 units, LDS fits at the layout's own row
+// format `sr`)
+static bool tile_parts(const qsc_obs_desc* d, int R, bool sr, int* np) {
+  const int nks = d->nks;
+  int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
+  const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
+  const bool fused = scfused_lds(d->PT, R, d->K, nks, 1, true) <= 160 * 1024;
+  while (NP > 1 && (chunks / NP < QSC_CPART_MIN_CHUNKS ||
+                    cpass_tile_lds(d->PT, R, nks, NP, true) > 160 * 1024 ||
+                    (fused && scfused_lds(d->PT, R, d->K, nks, NP, true) > 160 * 1024)))
+    --NP;
+  *np = NP;
+  return QSC_CPASS_TILE && nks * NP >= 4 && cpass_tile_lds(d->PT, R, nks, NP, sr) <= 160 * 1024;
 }
 
 // ---------------------------------------------------------------------------------------
