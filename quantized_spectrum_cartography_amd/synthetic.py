@@ -131,6 +131,115 @@ def ijslab_onebit_problem(I, J, K, R, rank, world, dist=None, f=0.1, seed=20260,
                 S0=S0.cpu(), C0=C0.cpu(), log_model=False, offset=0.0, thr=thr, T_true=T)
 
 
+def _orderable_keys(x):
+    """float32 -> int64 keys in [0, 2^32) whose integer order is the float order."""
+    bits = x.reshape(-1).contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    return torch.where(bits >= 0x80000000, 0xFFFFFFFF - bits, bits + 0x80000000)
+
+
+def _key_to_float(key):
+    import numpy as np
+    bits = key - 0x80000000 if key >= 0x80000000 else 0xFFFFFFFF - key
+    return float(np.array([bits], dtype=np.uint32).view(np.float32)[0])
+
+
+def global_kth(x, kth, dist=None):
+    """The kth smallest (0-based) float32 value of the union of every rank's `x` -- exactly,
+    without gathering the values: a two-digit (16 + 16 bit) radix select over the order-keyed
+    float bits, the 65536-bin histograms summed with two all-reduces.  With dist None, x is the
+    whole set; kth = (n - 1) // 2 is torch.median's lower median."""
+    key = _orderable_keys(x)
+    hi = key >> 16
+
+    def summed(h):
+        if dist is not None:
+            dist.all_reduce(h)
+        return h
+
+    h = summed(torch.bincount(hi, minlength=1 << 16))
+    cum = h.cumsum(0)
+    b_hi = int(torch.searchsorted(cum, torch.tensor([kth], device=cum.device), right=True)[0])
+    below = int(cum[b_hi - 1]) if b_hi > 0 else 0
+    lo = key[hi == b_hi] & 0xFFFF
+    h2 = summed(torch.bincount(lo, minlength=1 << 16))
+    cum2 = h2.cumsum(0)
+    b_lo = int(torch.searchsorted(cum2, torch.tensor([kth - below], device=cum2.device),
+                                  right=True)[0])
+    return _key_to_float((b_hi << 16) | b_lo)
+
+
+def _bin_seed(seed, k):
+    return int(seed) * 1000003 + 7919 * (int(k) + 1)
+
+
+def onebit_block_problem(I, J, K, R, k_range=None, i_range=None, f=0.1, seed=20260,
+                         device="cuda", dist=None, keep_T=True, reconstruct=None,
+                         quantizer=None):
+    """Bins [k0, k1) x image rows [i0, i1) of ONE global one-bit problem that is a function of
+    (seed, k) only, so a rank draws just its own block and the union of any split of the bins
+    (K-slab) or rows (IJ-slab) over any number of ranks is the same map -- with no rank ever
+    holding the whole map (C4: 268 M entries).
+
+    The BASELINE.md recipe, blocked: S_true = rand(R,1,I,J), C_true = rand(R,K), S0 = 0.5 rand,
+    C0 = 0.5 rand from one device generator (every rank draws the same small factors); the
+    noise and the Bernoulli(f) mask of bin k from a generator seeded by (seed, k);
+    T = get_tensor(S_true, C_true) on the block; thr = the exact lower median of the WHOLE map
+    (global_kth over the ranks' blocks, = torch.median of the union), sigma = (max - min)/4 of
+    the whole map (all-reduced), b = [0, thr, max]; Y = quantize(T, sigma, b).  `dist` must be
+    the process group whose blocks partition the map (None: this block is the whole map).
+    (`reconstruct` / `quantizer` replace get_tensor / quantize, for CPU tests of the blocking.)
+    Returns split_problem's keys: block C_true / C0 / Y / Wx / T_true, full S_true / S0 (row
+    block for i_range), plus "bounds" (k0, k1) and "rows" (i0, i1)."""
+    quantize = quantizer or _model.quantize
+    k0, k1 = k_range if k_range is not None else (0, K)
+    i0, i1 = i_range if i_range is not None else (0, I)
+    get_T = reconstruct or _model.get_tensor
+    g = torch.Generator(device=device).manual_seed(seed)
+    S_true = torch.rand(R, 1, I, J, generator=g, device=device)
+    C_true = torch.rand(R, K, generator=g, device=device)
+    S0 = 0.5 * torch.rand(R, 1, I, J, generator=g, device=device)
+    C0 = 0.5 * torch.rand(R, K, generator=g, device=device)
+    S_b, S0_b = S_true[..., i0:i1, :].contiguous(), S0[..., i0:i1, :].contiguous()
+    C_b, C0_b = C_true[:, k0:k1].contiguous(), C0[:, k0:k1].contiguous()
+    T = get_T(S_b, C_b)
+    ext = torch.stack([T.max(), -T.min()]).to(torch.float64)
+    if dist is not None:
+        dist.all_reduce(ext, op=dist.ReduceOp.MAX)
+    tmax, tmin = float(ext[0]), -float(ext[1])
+    thr = global_kth(T, (I * J * K - 1) // 2, dist)
+    sigma = (tmax - tmin) / 4
+    b = torch.tensor([0.0, thr, tmax])
+    noise = torch.empty((k1 - k0, i1 - i0, J), device=device)
+    Wx = torch.empty((k1 - k0, 1, i1 - i0, J), device=device)
+    full = torch.full((I, J), f, device=device)
+    for k in range(k0, k1):
+        gk = torch.Generator(device=device).manual_seed(_bin_seed(seed, k))
+        noise[k - k0] = torch.randn((I, J), generator=gk, device=device)[i0:i1]
+        Wx[k - k0, 0] = torch.bernoulli(full, generator=gk)[i0:i1]
+    Y = quantize(T, sigma, b, noise=noise).unsqueeze(1)
+    del noise
+    out = dict(S_true=S_b.cpu(), C_true=C_b.cpu(), b=b, sigma=sigma, Y=Y, Wx=Wx, S0=S0_b.cpu(),
+               C0=C0_b.cpu(), log_model=False, offset=0.0, thr=thr, bounds=(k0, k1),
+               rows=(i0, i1))
+    if keep_T:
+        out["T_true"] = T
+    return out
+
+
+def block_problem(cfg, rank, world, shard, seed, dist=None, device="cuda", **kw):
+    """This rank's share of the blocked global problem of a config (onebit_block_problem):
+    shard "kslab" = bins kslab_bounds(K, world, rank), "ijslab" = rows kslab_bounds(I, ...)."""
+    from .distributed import kslab_bounds
+    I, J, K, R = cfg
+    if shard == "kslab":
+        return onebit_block_problem(I, J, K, R, k_range=kslab_bounds(K, world, rank), seed=seed,
+                                    device=device, dist=dist, **kw)
+    if shard == "ijslab":
+        return onebit_block_problem(I, J, K, R, i_range=kslab_bounds(I, world, rank), seed=seed,
+                                    device=device, dist=dist, **kw)
+    raise ValueError("shard must be 'ijslab' or 'kslab'")
+
+
 def split_problem(prob, rank, world, shard):
     """This rank's shard of ONE global problem (strong scaling: the map is fixed, N ranks share
     it).  shard="ijslab": rows [i0, i1) of the I axis (pixels), C replicated; shard="kslab":

@@ -214,6 +214,25 @@ def test_mat_fixture_onebit_solve(golden):
     assert rel_fro(res.C.cpu().numpy(), ref["C"].numpy()) < 1e-5
 
 
+def test_solve_from_mat_file():
+    """Config 1 straight from the reference's .mat file (qmc_utils.onebit_problem_from_mat:
+    load_data + the notebook permutes, one-bit variant with the file's Om): GPU solve vs the
+    oracle's reference op sequence on the same arrays, 1e-5."""
+    import os
+    from quantized_spectrum_cartography_amd import qmc, qmc_utils
+    path = os.path.join(os.path.dirname(__file__), "golden", "onebitdata1.mat")
+    prob = qmc_utils.onebit_problem_from_mat(path)
+    R, K = prob["R"], prob["Y"].shape[0]
+    gen = torch.Generator().manual_seed(6)
+    S0 = 0.1 * torch.rand(R, 1, 51, 51, generator=gen)
+    C0 = 0.1 * torch.rand(R, K, generator=gen)
+    res = qmc.solve(prob["Y"], prob["Wx"], prob["b"], prob["sigma"], S_init=S0, C_init=C0,
+                    max_iter=5)
+    ref = osolver.free_s_solve(S0, C0, prob["Y"], prob["Wx"], prob["b"], prob["sigma"], n_iter=5)
+    assert rel_fro(res.S.cpu().numpy(), ref["S"].numpy()) < 1e-5
+    assert rel_fro(res.C.cpu().numpy(), ref["C"].numpy()) < 1e-5
+
+
 def test_generator_solver_vs_oracle():
     """GAN path (qmc/qmc.ipynb :541-634, config-1 setting: log model, 4 log bins, f = 0.1,
     sigma = 5, zero C, Z ~ N(0,1), random restart at i == 1) vs the oracle's loop with the same
