@@ -268,6 +268,29 @@ def split_problem(prob, rank, world, shard):
     return out
 
 
+def c5_problem(seed=5, I=256, K=64, R=4, f=0.1, sigma=5.0, device="cuda"):
+    """BASELINE configs[4]: a generated 256 x 256 x 64 map with R = 4
+    emitters (maps.generate_map: Gaussian PSDs, path loss x FFT-correlated shadowing, unit-norm
+    fields as generate_map.m:118), observed through the LOG model with the notebook's 4 log
+    bins, LOG_OFFSET_4 and sigma = 5 (qmc/qmc.ipynb :510-537), per-entry Bernoulli(f) mask
+    (:493).  S0 = (0.25 + 0.5 rand)/I (the fields' scale), C0 = 0.5 rand.  `lr_s` is the free-S
+    Adam step scaled to S (1e-5) so that T_hat = S C stays positive under the log model."""
+    from . import maps
+    from . import quantization_model_log as qml
+    from .utils import LOG_OFFSET_4, QUANTIZATION_BOUNDARIES_4_BINS_LOG
+    m = maps.generate_map(K, R, shadow_sigma=5.0, Xc=50.0, I=I, J=I, seed=seed, device=device)
+    g = torch.Generator().manual_seed(seed)
+    noise = torch.randn((K, I, I), generator=g)
+    b = torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG)
+    Y = qml.quantize(m["T"].cpu(), sigma, b, offset=LOG_OFFSET_4, noise=noise).unsqueeze(1)
+    Wx = torch.bernoulli(torch.full((K, 1, I, I), f), generator=g)
+    S0 = (0.25 + 0.5 * torch.rand(R, 1, I, I, generator=g)) / I
+    C0 = 0.5 * torch.rand(R, K, generator=g)
+    return dict(Y=Y, Wx=Wx, b=b, sigma=float(sigma), S0=S0, C0=C0,
+                S_true=m["S"].reshape(R, 1, I, I), C_true=m["C"], T_true=m["T"],
+                log_model=True, offset=LOG_OFFSET_4, lr_s=1e-5)
+
+
 CONFIGS = {
     # name: (I, J, K, R)   BASELINE.json configs
     "c2": (256, 256, 64, 4),
@@ -276,4 +299,6 @@ CONFIGS = {
     # one GPU's K-slab share of c4 at N = 8 (K_loc = 1024 / 8): the per-GPU kernel of the
     # north-star 8-GPU layout, benchable on one GPU
     "c4k": (512, 512, 128, 16),
+    # log model (4 log bins, sigma 5) on a generated map, free S (c5_problem)
+    "c5": (256, 256, 64, 4),
 }

@@ -88,21 +88,9 @@ def test_onebit_config_pass_and_solver(cfg, seed, fused):
 
 
 def _c5_problem(seed=5):
-    from quantized_spectrum_cartography_amd import maps
-    from quantized_spectrum_cartography_amd import quantization_model_log as qml
-    from quantized_spectrum_cartography_amd.utils import (LOG_OFFSET_4,
-                                                          QUANTIZATION_BOUNDARIES_4_BINS_LOG)
-    K, R, I = 64, 4, 256
-    m = maps.generate_map(K, R, shadow_sigma=5.0, Xc=50.0, I=I, J=I, seed=seed)
-    g = torch.Generator().manual_seed(seed)
-    noise = torch.randn((K, I, I), generator=g)
-    b = torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG)
-    Y = qml.quantize(m["T"].cpu(), 5.0, b, offset=LOG_OFFSET_4, noise=noise).unsqueeze(1)
-    Wx = torch.bernoulli(torch.full((K, 1, I, I), 0.1), generator=g)
-    S0 = (0.25 + 0.5 * torch.rand(R, 1, I, I, generator=g)) / I
-    C0 = 0.5 * torch.rand(R, K, generator=g)
-    prob = dict(Y=Y, Wx=Wx, b=b, sigma=5.0, S0=S0, C0=C0, S_true=m["S"], T_true=m["T"])
-    return prob, (I, I, K, R), LOG_OFFSET_4
+    from quantized_spectrum_cartography_amd import synthetic
+    prob = synthetic.c5_problem(seed=seed)
+    return prob, (256, 256, 64, 4), prob["offset"]
 
 
 def test_c5_log_model_pass_and_solver():
