@@ -165,7 +165,7 @@ class _CpuEngine:
         return dict(self.st)
 
 
-def _problem():
+def _problem(K=K):
     g = torch.Generator().manual_seed(11)
     S_true = torch.rand(R, 1, I, J, generator=g)
     C_true = torch.rand(R, K, generator=g)
@@ -204,9 +204,9 @@ class _SoloDist:
         out.copy_(t)
 
 
-def _run(dist_mod, rank, world):
+def _run(dist_mod, rank, world, K=K):
     from quantized_spectrum_cartography_amd.distributed import KSlabSolver, kslab_bounds
-    S0, C0, Y, Wx, b, sigma = _problem()
+    S0, C0, Y, Wx, b, sigma = _problem(K)
     k0, k1 = kslab_bounds(K, world, rank)
     obs = _Obs(Y[k0:k1], Wx[k0:k1])
     eng = _CpuEngine(obs, b.numpy(), sigma)
@@ -234,11 +234,11 @@ def _run_ij(dist_mod, rank, world):
     return sol.S_pixels().reshape(R, -1), sol.C.clone(), eng.read_state()
 
 
-def _worker(rank, world, port, out_path, mode):
+def _worker(rank, world, port, out_path, mode, K_=K):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        S, C, st = (_run if mode == "k" else _run_ij)(dist, rank, world)
+        S, C, st = (_run(dist, rank, world, K_) if mode == "k" else _run_ij(dist, rank, world))
         np.savez(out_path + ".r%d" % rank, S=S.numpy(), C=C.numpy(), step_s=st["step_s"],
                  shard=np.array(st.get("shard", (0, 0))))
     finally:
@@ -284,6 +284,32 @@ def test_kslab_two_ranks_match_single_process(tmp_path):
     ref = osolver.free_s_solve(S0, C0, Y, Wx, b, sigma, n_iter=ITERS)
     assert rel_fro(two["S"], ref["S"].reshape(R, -1).numpy()) < 1e-5
     assert rel_fro(two["C"], ref["C"].numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("world,K_", [(3, 17), (4, 18)])
+def test_kslab_uneven_ranks_match_single_process(tmp_path, world, K_):
+    """K-slab over 3 and 4 ranks with uneven bin splits (17 = 6 + 6 + 5, 18 = 5 + 5 + 4 + 4)
+    and position shards of unequal content: the same S, C as one process over all bins, and
+    the reference op sequence within the parity tolerance."""
+    from quantized_spectrum_cartography_amd.distributed import kslab_bounds
+    out = str(tmp_path / "ku")
+    mp.start_processes(_worker, args=(world, _free_port(), out, "k", K_), nprocs=world,
+                       join=True, start_method="spawn")
+    res = [np.load(out + ".r%d.npz" % r) for r in range(world)]
+    sizes = [b_ - a for a, b_ in (kslab_bounds(K_, world, r) for r in range(world))]
+    assert len(set(sizes)) == 2  # uneven
+    for r in res[1:]:
+        assert np.array_equal(r["S"], res[0]["S"]) and np.array_equal(r["C"], res[0]["C"])
+    shards = [tuple(r["shard"]) for r in res]
+    assert shards[0][0] == 0 and shards[-1][1] == I * J
+    assert all(a[1] == b_[0] for a, b_ in zip(shards, shards[1:]))
+    S1, C1, _ = _run(_SoloDist, 0, 1, K_)
+    assert rel_fro(res[0]["S"], S1.numpy()) < 1e-6
+    assert rel_fro(res[0]["C"], C1.numpy()) < 1e-6
+    S0, C0, Y, Wx, b, sigma = _problem(K_)
+    ref = osolver.free_s_solve(S0, C0, Y, Wx, b, sigma, n_iter=ITERS)
+    assert rel_fro(res[0]["S"], ref["S"].reshape(R, -1).numpy()) < 1e-5
+    assert rel_fro(res[0]["C"], ref["C"].numpy()) < 1e-5
 
 
 def test_ijslab_two_ranks_match_single_process(tmp_path):

@@ -273,6 +273,41 @@ def test_generator_solver_vs_oracle():
     assert np.allclose(res.costs_s, ref["costs_s"], rtol=1e-4)
 
 
+def test_dip_solver_vs_oracle():
+    """dip.solve end to end (optimize="weights": Adam on the decoder weights, Z fixed; the
+    reference's DecoderDip, deep_prior/networks/dip.py:20-89, at 51 x 51; log model, 4 log bins,
+    sigma 5, f = 0.1 as qmc/qmc.ipynb :510-537) vs the oracle's reference-formulation loop
+    (oracle/solver.py dip_solve: CPU autograd through masked_nll and the decoder) with the same
+    BN-calibrated decoder.  As for the GAN path, the torch decoder itself runs on MIOpen vs CPU
+    convs, so the tolerance is 1e-4."""
+    import copy
+    from quantized_spectrum_cartography_amd import dip, nets
+    from quantized_spectrum_cartography_amd.utils import LOG_OFFSET_4, QUANTIZATION_BOUNDARIES_4_BINS_LOG
+    torch.manual_seed(0)
+    R, K = 2, 64
+    dec = nets.DecoderDip()
+    Z0 = torch.randn(R, 256)
+    dip.calibrate_bn(dec, Z0)  # (CPU, once: both sides start from the same weights and stats)
+    S_true = torch.rand(R, 1, 51, 51) ** 4 * 0.2
+    C_true = torch.rand(R, K)
+    Tt = ro.get_tensor(S_true, C_true)
+    b = torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG)
+    Y = ro.quantize(Tt, 5.0, b, offset=LOG_OFFSET_4, log_model=True).unsqueeze(1)
+    Wx = torch.bernoulli(torch.full((K, 1, 51, 51), 0.1))
+    C0 = 0.05 * torch.rand(R, K)
+    # (a decoder step of lr 1e-3 keeps the 4 iterations smooth: at 1e-2 the fresh decoder's
+    # first steps jump the cost by 70 %, where last-bit conv differences are amplified)
+    ref = osolver.dip_solve(copy.deepcopy(dec).eval(), Z0, C0, Y, Wx, b, 5.0, LOG_OFFSET_4, True,
+                            n_iter=4, lr_s=1e-3)
+    res = dip.solve(Y, Wx, b, 5.0, R, offset=LOG_OFFSET_4, decoder=copy.deepcopy(dec).cuda(),
+                    Z_init=Z0, C_init=C0, max_iter=4, lr_s=1e-3)
+    assert res.S.shape == (R, 1, 51, 51)
+    assert rel_fro(res.S.cpu().numpy(), ref["S"].numpy()) < 1e-4
+    assert rel_fro(res.C.cpu().numpy(), ref["C"].numpy()) < 1e-4
+    assert np.allclose(res.costs_c, ref["costs_c"], rtol=1e-4)
+    assert np.allclose(res.costs_s, ref["costs_s"], rtol=1e-4)
+
+
 def test_dip_solver_256():
     from quantized_spectrum_cartography_amd import dip
     from quantized_spectrum_cartography_amd.utils import QUANTIZATION_BOUNDARIES_4_BINS_LOG
