@@ -66,19 +66,22 @@ def free_s_solve(S0, C0, Y, Wx, b, sigma, offset=0.0, log_model=False, n_iter=10
 
 
 def dip_solve(decoder, Z, C0, Y, Wx, b, sigma, offset=0.0, log_model=True, n_iter=4,
-              lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2):
-    """The DIP variant of the loop (quantized_spectrum_cartography_amd.dip.solve, optimize=
-    "weights": the reference's empty qmc/dip.py defined on the GAN loop of qmc/qmc.ipynb
-    :541-634 with S = decoder(Z) and Adam on the decoder weights, Z fixed) in the reference
-    formulation: torch CPU autograd through masked_nll and the decoder, torch.optim.Adam.  The
-    S-step cost keeps the notebook's lambda_s ||Z||_F term (a constant here).  Costs as the
-    GAN loop's (cost.item() before each step)."""
+              lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2, optimize="weights"):
+    """The DIP variant of the loop (quantized_spectrum_cartography_amd.dip.solve: the
+    reference's empty qmc/dip.py defined on the GAN loop of qmc/qmc.ipynb :541-634 with
+    S = decoder(Z); optimize="weights": Adam on the decoder weights, Z fixed; "z": Adam on Z,
+    the weights fixed, as the GAN loop) in the reference formulation: torch CPU autograd
+    through masked_nll and the decoder, torch.optim.Adam.  The S-step cost keeps the
+    notebook's lambda_s ||Z||_F term.  Costs as the GAN loop's (cost.item() before each
+    step)."""
     R = Z.shape[0]
     I, J = Y.shape[-2], Y.shape[-1]
     C = C0.clone().requires_grad_(True)
-    Zc = Z.clone()
+    Zc = Z.clone().requires_grad_(optimize == "z")
     optC = torch.optim.Adam([C], lr=lr_c)
-    optS = torch.optim.Adam(list(decoder.parameters()), lr=lr_s)
+    for p in decoder.parameters():
+        p.requires_grad_(optimize == "weights")
+    optS = torch.optim.Adam([Zc] if optimize == "z" else list(decoder.parameters()), lr=lr_s)
     with torch.no_grad():
         S = decoder(Zc).reshape(R, 1, I, J)
     costs_c, costs_s = [], []
