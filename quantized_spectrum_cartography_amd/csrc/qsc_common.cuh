@@ -502,6 +502,31 @@ __device__ __forceinline__ T block_sum(T v, T* sh) {
   return r;  // valid in thread 0
 }
 
+// The same sums for a caller-supplied thread index `tid` (== threadIdx.x): the lane indices of
+// the shuffles derive from it, so that a persistent kernel which re-derives `tid` each iteration
+// keeps them from being hoisted out of its loop (and spilled); ds_bpermute is what __shfl_xor
+// issues at width 64, hence the same values bit for bit
+__device__ __forceinline__ float wave_sum_tid(float v, unsigned tid) {
+  const int lane = (int)(tid & 63);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    v += __int_as_float(__builtin_amdgcn_ds_bpermute((lane ^ o) << 2, __float_as_int(v)));
+  return v;
+}
+__device__ __forceinline__ float block_sum_tid(float v, float* sh, unsigned tid) {
+  v = wave_sum_tid(v, tid);
+  const int w = (int)(tid >> 6), l = (int)(tid & 63);
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  float r = 0;
+  if (tid == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int i = 0; i < nw; ++i) r += sh[i];
+  }
+  return r;  // valid in thread 0
+}
+
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 __host__ __device__ inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
 

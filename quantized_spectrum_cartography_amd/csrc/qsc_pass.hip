@@ -1465,13 +1465,13 @@ size_t cpass_tile_lds(int PT, int R, int nks, int NP, bool sr) {
 // ---------------------------------------------------------------------------------------
 // fused launch block: 16 waves (4 per SIMD, 128 VGPRs) up to rank 8; 8 waves at rank 16, whose
 // two slice register sets and 16-float rows need up to 256 VGPRs (2 waves per SIMD)
-// Stores of the values the fused finish's tail reads (qsc_scpass_fin: dC slab rows, NLL / norm
-// partials, the state's book-keeping fields): with FIN they are agent-scope relaxed atomic
-// stores, i.e. written through this XCD's L2 to the device coherence point, so that the
-// finishing workgroups on other XCDs see them once the stores have completed (s_waitcnt) --
-// no L2 write-back fence per workgroup (measured: with one `buffer_wbl2` per workgroup the
-// launch took 40 us against 31 + 3 for the launch pair).  Without FIN: plain stores.
-// ... and their loads in the finishing workgroups: agent-scope relaxed atomic loads (sc1, served
+// Stores of the values other workgroups of the persistent loop read within the launch
+// (qsc_scpass_loop: dC slab rows, NLL / norm partials): with FIN they are agent-scope relaxed
+// atomic stores, i.e. written through this XCD's L2 to the device coherence point, so that
+// workgroups on other XCDs see them once the stores have completed (s_waitcnt) -- no L2
+// write-back fence per workgroup (measured in round 4: with one `buffer_wbl2` per workgroup a
+// one-launch iteration took 40 us against 31 + 3 for the launch pair).  Without FIN: plain
+// stores.  ... and their loads in the reading workgroups: agent-scope relaxed atomic loads (sc1, served
 // by the XCD's L2, never by the CU's L1), so that with write-through stores on the producer side
 // and the vmcnt-drained ticket no acquire fence is needed (MI355X_MICROARCH.md, hand-off forms:
 // every load of the handed-off bytes sc1, every store sc1, one lane signalling behind a barrier)
@@ -1518,27 +1518,37 @@ struct FusedBlock {
       qsc_state *__restrict__ st, float *__restrict__ part_nll_s, float *__restrict__ part_nsq_s, \
       float *__restrict__ slab, float *__restrict__ part_nll_c, float *__restrict__ cnsq,         \
       AdamCache *__restrict__ acache, const int *__restrict__ c_split
-// scfin_kernel's form: C is written by its C-finish tail, so the kernel parameter carries no
-// __restrict__ (the tile body's restrict-qualified read-only view is scoped to scfused_tile,
-// which finishes every read of C before the tail writes it)
-#define QSC_SCFIN_KPARAMS                                                                      \
-  const E *__restrict__ s_ent, const int *__restrict__ s_width, const int64_t *__restrict__ s_off, \
-      const E *__restrict__ c_ent, const int *__restrict__ c_width,                                \
-      const int64_t *__restrict__ c_off, const int *__restrict__ c_kmap, int nks, int NP, int PT,  \
-      Lik lk, Edges E_, int nbins, int R, int K, float *__restrict__ S, float *C,                 \
-      float *__restrict__ mS, float *__restrict__ vS, qsc_adam ad, float lambda_s,                \
-      qsc_state *__restrict__ st, float *__restrict__ part_nll_s, float *__restrict__ part_nsq_s, \
-      float *__restrict__ slab, float *__restrict__ part_nll_c, float *__restrict__ cnsq,         \
-      AdamCache *__restrict__ acache, const int *__restrict__ c_split
 #define QSC_SCF_ARGS                                                                            \
   s_ent, s_width, s_off, c_ent, c_width, c_off, c_kmap, nks, NP, PT, lk, E_, nbins, R, K, S, C, mS, \
       vS, ad, lambda_s, st, part_nll_s, part_nsq_s, slab, part_nll_c, cnsq, acache, c_split
 
-// One pixel tile t of nt of the fused launch (scfused_kernel, scfin_kernel: t = the workgroup).
-// C is read-only here; scfin_kernel's C-finish writes it after every tile has finished.
-template <int RP, typename E, int KIND, bool LOG, bool FIN = false>
+// The persistent loop's per-workgroup state in LDS (scloop_kernel, after the tile's LDS): the
+// solver state as the launch pairs would leave it in qsc_state (every workgroup keeps its own,
+// identical copy; workgroup 0 writes it back at the end), the next iteration's Adam scalars,
+// the C-step scalars of the head, and the tile's per-slice / per-k-slice NLL and ||S||^2
+// partials for its canonical tile sums (canon_totals).
+struct LoopState {
+  int step_s, step_c, iter, pending;
+  float normsq_s, normsq_c, nll_c, nll_s, normsq_s_prev;
+  int fault, last, pad_;
+  AdamScalars as_s, as_c;  // the next iteration's S-step / C-step Adam scalars
+  Scalars scc;             // the head's C-step regulariser coefficient and Adam scalars
+  float sh[16];            // block_sum scratch of the head
+  float ts[1];             // [2 nsl] per-slice NLL, ||S||^2; then [nks] per-k-slice C-pass NLL
+};
+size_t loop_lds(int nsl, int nks) {
+  return (sizeof(LoopState) + (size_t)(2 * nsl + nks) * 4 + 15) & ~(size_t)15;
+}
+
+// One pixel tile t of nt of the fused launch (scfused_kernel; scloop_kernel: t = the workgroup).
+// C is read-only here.  LOOP (scloop_kernel): every cross-workgroup value is stored write-through
+// (FIN), qsc_state is not touched (the state lives in `ll`), the tile's scalar partials also go to
+// `ll`; with `head` the caller has already staged the new C^T and the S-step scalars (iterations
+// after the first: the LDS tables' static parts stay from the first).
+template <int RP, typename E, int KIND, bool LOG, bool FIN = false, bool LOOP = false>
 __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const int nt,
-                                             const unsigned tidx) {
+                                             const unsigned tidx, const bool head = false,
+                                             LoopState* ll = nullptr) {
   using V4 = typename Ent<E>::V4;
   constexpr int CP = TP<RP, KIND>::v;  // C^T row pitch == S tile row pitch
   constexpr int RH = RP / 2;
@@ -1571,6 +1581,8 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   // 1. C^T / edge / state reads first (the LDS staging then waits only for them: vmcnt
   //    retires in issue order), then the first slice's reads, then the staging
   const int k0 = tidx;
+  // LOOP iterations after the first: C^T, the tables' static parts and the scalars are staged
+  const bool stage_c = !(LOOP && head);
 #if QSC_CT_VEC
   // C^T from 16-B reads of the [R][K] C: thread i holds C's flat floats 4i..4i+3 (one row r,
   // four consecutive bins) and writes them transposed; 32x fewer read instructions than a
@@ -1579,7 +1591,10 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   const bool cvec = (K & 3) == 0 && ((reinterpret_cast<uintptr_t>(C) & 15) == 0);
   float4 cq = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   float c0[RP];
-  if (cvec) {
+  if (!stage_c) {
+#pragma unroll
+    for (int r = 0; r < RP; ++r) c0[r] = 0.0f;
+  } else if (cvec) {
     cq = reinterpret_cast<const float4*>(C)[min(k0, n4 - 1)];
   } else {
 #pragma unroll
@@ -1606,7 +1621,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   float nsq_s = 0.0f;
   int step_s = 0;
   AdamCache ac0{}, ac1{};
-  if (tidx == 0) {
+  if (tidx == 0 && stage_c) {
     nsq_s = st->normsq_s;
     step_s = st->step_s;
     ac0 = acache[0];  // both slots: no dependent read on step_s
@@ -1622,6 +1637,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   // burst is then a quarter of the tile's slice data and the S-step starts that much earlier.
   const bool early = w < QSC_EARLY_WAVES;
   auto stage = [&]() {
+    if (!stage_c) return;  // (LOOP, after the first iteration: staged by the head)
 #if QSC_CT_VEC
     if (cvec) {
       const int Ko = sr_off(K);  // the negated half of a signed-row C^T table
@@ -1681,7 +1697,21 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
       const float nrm = sqrtf(nsq_s);
       sc.coef = nrm > 0.0f ? lambda_s / nrm : 0.0f;
       sc.as = adam_scalars_cached(((step_s + 1) & 1) ? ac1 : ac0, ad, step_s + 1);
-      if (t == 0) {
+      if constexpr (LOOP) {
+        // the state after this S-step's start (what t == 0 stores in the launch form below),
+        // kept by every workgroup; workgroup 0 writes it back at the end of the loop
+        const int pend = st->pending;
+        ll->step_s = step_s;
+        ll->step_c = st->step_c + ((pend & QSC_PEND_C) ? 1 : 0);
+        ll->pending = (pend & ~QSC_PEND_C) | QSC_PEND_SNLL | QSC_PEND_SUPD;
+        ll->normsq_s = nsq_s;
+        ll->normsq_s_prev = nsq_s;
+        ll->iter = st->iter + 1;
+        ll->nll_c = st->nll_c;
+        ll->nll_s = st->nll_s;
+        ll->normsq_c = st->normsq_c;
+        ll->fault = 0;
+      } else if (t == 0) {
         // book-keeping of spass_kernel (mode 1)
         int pend = st->pending;
         if (pend & QSC_PEND_C) st_fin<FIN>(&st->step_c, st->step_c + 1);
@@ -1713,7 +1743,8 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
         const float c = Cl[k * CP + r];
         s2 = __builtin_fmaf(c, c, s2);
       }
-    const float nsq = block_sum(s2, Nl);
+    // (the same sum either way; the loop's form keeps its lane indices in the iteration)
+    const float nsq = LOOP ? block_sum_tid(s2, Nl, tidx) : block_sum(s2, Nl);
     if (tidx == 0) st_fin<FIN>(cnsq, nsq);
   }
 
@@ -1777,6 +1808,12 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     if (lane == 0) st_fin<FIN>(&part_nsq_s[s], nsq);
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (lane == 0) st_fin<FIN>(&part_nll_s[s], nll_w);
+    if constexpr (LOOP) {
+      if (lane == 0) {
+        ll->ts[il] = nll_w;
+        ll->ts[nsl + il] = nsq;
+      }
+    }
     STAMP(wg, 5 + min(n, 8));  // end of the wave's n-th slice
     il = il1;
     ++n;
@@ -1872,7 +1909,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
 
   // the next launch's S-step scalars, by the oldest wave of block 0 (it has slack: its slices
   // are done long before the tile barrier)
-  if (t == 0 && tidx == 0) adam_cache_store<FIN>(acache, ad, step_s + 2);
+  if (!LOOP && t == 0 && tidx == 0) adam_cache_store<FIN>(acache, ad, step_s + 2);
 
   STAMP(wg, 2);
   if (u < U) {
@@ -1893,6 +1930,9 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
         if (2 * j + 1 < R) st_fin<FIN>(&slab[((int64_t)t * R + 2 * j + 1) * Kp + k], accp[j].y);
       }
       if (lane == 0) st_fin<FIN>(&part_nll_c[wi], nll_w);
+      if constexpr (LOOP) {
+        if (lane == 0) ll->ts[2 * nsl + u] = nll_w;  // (NP == 1: unit u is k-slice u)
+      }
     } else {
       to_pl(accp);
       if (lane == 0) Nl[u] = nll_w;
@@ -1919,6 +1959,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
       float acc = Nl[ks * NP];
       for (int pp = 1; pp < NP; ++pp) acc += Nl[ks * NP + pp];
       st_fin<FIN>(&part_nll_c[t * nks + ks], acc);
+      if constexpr (LOOP) ll->ts[2 * nsl + ks] = acc;
     }
   }
   STAMP(wg, kStampLast);
@@ -1956,31 +1997,104 @@ static bool tile_parts(const qsc_obs_desc* d, int R, bool sr, int* np) {
 }
 
 // ---------------------------------------------------------------------------------------
-// book-keeping shared by cfinish (block 0) and state_flush: settle a pending S-pass
+// The canonical order of the scalar partials -- the S-passes' per-slice NLL and ||S||^2
+// (part_nll_s, part_nsq_s) and the C-passes' per-(tile, k-slice) NLL (part_nll_c).  Every form
+// settles them in this ONE order, so that the launch pairs (cfinish, state_flush) and the
+// persistent loop (whose tiles, tile groups and workgroups form these sums where the partials
+// are produced: scloop_kernel) agree bit for bit:
+//   tile t:   its items in order (slices slice_of(l, t), l = 0 .. nsl-1; k-slices 0 .. nks-1)
+//   group g:  the tile sums of tiles g, g + kTGroups, g + 2 kTGroups, ... in order
+//   total:    the kTGroups group sums in g order
+// every sum starting from +0.  The groups are the C-finish's tile classes (cfinish sums a dC
+// column over tiles vw, vw + 16, ... per virtual wave vw, then the 16 in order).
 // ---------------------------------------------------------------------------------------
+constexpr int kTGroups = 16;
+__host__ __device__ __forceinline__ int slice_of(int l, int t, int nt) {
+  return l * nt + ((l & 1) ? (nt - 1 - t) : t);
+}
+struct Canon {
+  float nll_s, nsq_s, nll_c;
+};
+
+// The three canonical totals, by one workgroup of any size >= kTGroups; ts: LDS [3][blockDim],
+// gs: LDS [3][kTGroups].  Result valid in thread 0.
+__device__ Canon canon_totals(const float* __restrict__ nll_s, const float* __restrict__ nsq_s,
+                              const float* __restrict__ nll_c, int ntiles, int nsl, int nks,
+                              float* ts, float* gs) {
+  const int nb = blockDim.x, tid = threadIdx.x;
+  float ga = 0.0f, gb = 0.0f, gc = 0.0f;  // thread g < kTGroups: running group sums
+  for (int t0 = 0; t0 < ntiles; t0 += nb) {
+    const int t = t0 + tid;
+    if (t < ntiles) {
+      // the tile's items, every load issued before the in-order sums
+      float a = 0.0f, b = 0.0f, c = 0.0f;
+      for (int l0 = 0; l0 < nsl; l0 += 8) {
+        float va[8], vb[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int s = slice_of(min(l0 + j, nsl - 1), t, ntiles);
+          va[j] = nll_s ? nll_s[s] : 0.0f;
+          vb[j] = nsq_s ? nsq_s[s] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (l0 + j < nsl) {
+            a += va[j];
+            b += vb[j];
+          }
+      }
+      if (nll_c)
+        for (int ks = 0; ks < nks; ++ks) c += nll_c[(int64_t)t * nks + ks];
+      ts[tid] = a;
+      ts[nb + tid] = b;
+      ts[2 * nb + tid] = c;
+    }
+    __syncthreads();
+    if (tid < kTGroups) {
+      const int end = min(t0 + nb, ntiles);
+      for (int t1 = t0 + ((tid - t0 % kTGroups) + kTGroups) % kTGroups; t1 < end; t1 += kTGroups) {
+        ga += ts[t1 - t0];
+        gb += ts[nb + t1 - t0];
+        gc += ts[2 * nb + t1 - t0];
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < kTGroups) {
+    gs[tid] = ga;
+    gs[kTGroups + tid] = gb;
+    gs[2 * kTGroups + tid] = gc;
+  }
+  __syncthreads();
+  Canon r{0.0f, 0.0f, 0.0f};
+  if (tid == 0)
+    for (int g = 0; g < kTGroups; ++g) {
+      r.nll_s += gs[g];
+      r.nsq_s += gs[kTGroups + g];
+      r.nll_c += gs[2 * kTGroups + g];
+    }
+  return r;
+}
+
+// book-keeping shared by cfinish (block 0) and state_flush: settle a pending S-pass
 __device__ void settle_s(qsc_state* __restrict__ st, const float* __restrict__ part_nll_s,
-                         const float* __restrict__ part_nsq_s, int nslices, float* hist,
-                         int hist_cap, float* sh) {
+                         const float* __restrict__ part_nsq_s, int ntiles, int nsl, float* hist,
+                         int hist_cap, float* ts, float* gs) {
   const int pend = st->pending;  // uniform read (all threads)
   if (!(pend & (QSC_PEND_SNLL | QSC_PEND_SUPD))) return;
-  float a = 0.0f, b = 0.0f;
-  for (int i = threadIdx.x; i < nslices; i += blockDim.x) {
-    a += part_nll_s[i];
-    if (pend & QSC_PEND_SUPD) b += part_nsq_s[i];
-  }
-  const float nll = block_sum(a, sh);
-  const float nsq = block_sum(b, sh);
+  const Canon c = canon_totals(part_nll_s, (pend & QSC_PEND_SUPD) ? part_nsq_s : nullptr, nullptr,
+                               ntiles, nsl, 0, ts, gs);
   if (threadIdx.x == 0) {
     const int it = st->iter - 1;
-    st->nll_s = nll;
+    st->nll_s = c.nll_s;
     if (hist && it >= 0 && it < hist_cap) {
       hist[4 * it + 0] = st->nll_c;
-      hist[4 * it + 1] = nll;
+      hist[4 * it + 1] = c.nll_s;
       hist[4 * it + 2] = st->normsq_c;
       hist[4 * it + 3] = st->normsq_s_prev;
     }
     if (pend & QSC_PEND_SUPD) {
-      st->normsq_s = nsq;
+      st->normsq_s = c.nsq_s;
       st->step_s += 1;
     }
     st->pending = pend & ~(QSC_PEND_SNLL | QSC_PEND_SUPD);
@@ -2048,16 +2162,15 @@ __device__ __forceinline__ void cfin_tile_sum(float (*red)[64], const float* col
     if (wave + f * NWp < NW) red[wave + f * NWp][lane] = a[f];
 }
 
-// C-finish work item vb of R*nks + 2 (cfinish_kernel: vb = the workgroup; scfin_kernel: one
-// item per late-arriving workgroup), with its LDS scratch passed in.  The sums are those of a
-// 16-wave workgroup (kFWaves partial sums per column, in wave order); a smaller workgroup (the
-// fused finish of a 4..15-wave fused launch, DEV) runs them as virtual waves vw = wave,
-// wave + NWp, ... (at most 4 per physical wave, cfin_tile_sum), same operands in the same order.
-template <bool DEV = false>
+// C-finish work item vb of R*nks + 2 (cfinish_kernel: vb = the workgroup), with its LDS scratch
+// passed in: per (r, 64-bin slice) column block the 16 waves' partials (wave w: tiles w, w + 16,
+// ... in order -- the canonical tile groups, canon_totals) summed in wave order; item R*nks the
+// book-keeping (canon_totals), item R*nks + 1 the next C-step's Adam scalars.
+constexpr bool DEV = false;
 __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scalars& sc,
-                                           float (*sh3)[kFWaves], QSC_CF_PARAMS) {
+                                           float* ts, float* gs, QSC_CF_PARAMS) {
   constexpr int NW = kFWaves;
-  const int NWp = DEV ? (int)(blockDim.x >> 6) : NW;
+  const int NWp = NW;
   const int Kp = nks * 64;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 
@@ -2071,71 +2184,35 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
     return;
   }
   if (vb == R * nks) {
-    // book-keeping block: settle the S-pass partials (settle_s) and total the C-pass NLL.
-    // Every partial is read up front (one memory round trip, batches of 8 loads in flight)
-    // and the three fixed-order block sums share one LDS pass; same sums, same order as
-    // settle_s + block_sum.
-    const int pend = ld_fin<DEV>(&st->pending);
+    // book-keeping block: settle the S-pass partials (settle_s) and total the C-pass NLL, in
+    // the canonical order (canon_totals)
+    const int pend = st->pending;
     const bool settle = (pend & (QSC_PEND_SNLL | QSC_PEND_SUPD)) != 0;
     const bool supd = (pend & QSC_PEND_SUPD) != 0;
-    constexpr int step = kFBlock;
-    for (int vw = wave; vw < NW; vw += NWp) {
-      const int vt = vw * 64 + lane;
-      float a = 0.0f, b = 0.0f, c = 0.0f;
-      for (int i0 = vt; settle && i0 < nslices; i0 += 8 * step) {
-        float va[8], vb[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int i = min(i0 + j * step, nslices - 1);
-          va[j] = ld_fin<DEV>(&part_nll_s[i]);
-          vb[j] = supd ? ld_fin<DEV>(&part_nsq_s[i]) : 0.0f;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (i0 + j * step < nslices) {
-            a += va[j];
-            if (supd) b += vb[j];
-          }
-      }
-      for (int i = vt; i < npart_c; i += step) c += ld_fin<DEV>(&part_nll_c[i]);
-      a = wave_sum(a);
-      b = wave_sum(b);
-      c = wave_sum(c);
-      if (lane == 0) {
-        sh3[0][vw] = a;
-        sh3[1][vw] = b;
-        sh3[2][vw] = c;
-      }
-    }
-    __syncthreads();
+    const Canon cs = canon_totals(settle ? part_nll_s : nullptr, supd ? part_nsq_s : nullptr,
+                                  part_nll_c, ntiles, nslices / ntiles, nks, ts, gs);
     if (threadIdx.x == 0) {
-      float sn = 0.0f, sq = 0.0f, tot = 0.0f;
-      for (int w = 0; w < NW; ++w) {
-        sn += sh3[0][w];
-        sq += sh3[1][w];
-        tot += sh3[2][w];
-      }
       int pnd = pend;
       if (settle) {  // settle_s, thread-0 part
-        const int it = ld_fin<DEV>(&st->iter) - 1;
-        st_fin<DEV>(&st->nll_s, sn);
+        const int it = st->iter - 1;
+        st->nll_s = cs.nll_s;
         if (hist && it >= 0 && it < hist_cap) {
-          hist[4 * it + 0] = ld_fin<DEV>(&st->nll_c);
-          hist[4 * it + 1] = sn;
-          hist[4 * it + 2] = ld_fin<DEV>(&st->normsq_c);
-          hist[4 * it + 3] = ld_fin<DEV>(&st->normsq_s_prev);
+          hist[4 * it + 0] = st->nll_c;
+          hist[4 * it + 1] = cs.nll_s;
+          hist[4 * it + 2] = st->normsq_c;
+          hist[4 * it + 3] = st->normsq_s_prev;
         }
         if (supd) {
-          st_fin<DEV>(&st->normsq_s, sq);
-          st_fin<DEV>(&st->step_s, ld_fin<DEV>(&st->step_s) + 1);
+          st->normsq_s = cs.nsq_s;
+          st->step_s += 1;
         }
         pnd = pend & ~(QSC_PEND_SNLL | QSC_PEND_SUPD);
-        st_fin<DEV>(&st->pending, pnd);
+        st->pending = pnd;
       }
-      st_fin<DEV>(&st->nll_c, tot);
+      st->nll_c = cs.nll_c;
       if (mode == 1) {
-        st_fin<DEV>(&st->normsq_c, nsq);
-        st_fin<DEV>(&st->pending, pnd | QSC_PEND_C);
+        st->normsq_c = nsq;
+        st->pending = pnd | QSC_PEND_C;
       }
       if (mode == 2) dC[(int64_t)R * K] = st->normsq_s;  // this shard's ||S||^2 (IJ-slab)
     }
@@ -2162,12 +2239,7 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
   // tile sum: (virtual) wave w takes tiles w, w+16, ...; sixteen independent loads in flight
   const float* col = slab + (int64_t)r * Kp + k;
   const int64_t tstride = (int64_t)R * Kp;
-  if (!DEV || NWp >= NW)
-    cfin_tile_sum<DEV, 1>(red, col, tstride, ntiles, wave, NWp, lane);
-  else if (2 * NWp >= NW)
-    cfin_tile_sum<DEV, 2>(red, col, tstride, ntiles, wave, NWp, lane);
-  else
-    cfin_tile_sum<DEV, 4>(red, col, tstride, ntiles, wave, NWp, lane);
+  cfin_tile_sum<DEV, 1>(red, col, tstride, ntiles, wave, NWp, lane);
   __syncthreads();
   if (wave == 0 && k < K) {
     float g = red[0][lane];
@@ -2190,135 +2262,44 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
 __global__ void __launch_bounds__(kFBlock) cfinish_kernel(QSC_CF_PARAMS) {
   __shared__ float red[kFWaves][64];
   __shared__ Scalars sc;
-  __shared__ float sh3[3][kFWaves];
-  cfinish_vb((int)blockIdx.x, red, sc, sh3, QSC_CF_ARGS);
+  __shared__ float ts[3 * kFBlock];
+  __shared__ float gs[3 * kTGroups];
+  cfinish_vb((int)blockIdx.x, red, sc, ts, gs, QSC_CF_ARGS);
 }
 
 // ---------------------------------------------------------------------------------------
-// Fused launch with the C-finish at its tail (qsc_scpass_fin)
+// Persistent fused loop (qsc_scpass_loop): n fused bodies -- S-step i + C-pass i+1, and the
+// C-step finish of that C-pass -- in ONE launch, one workgroup per C-pass tile for the whole
+// launch (every workgroup resident: the launcher checks occupancy x CUs >= tiles).  No
+// workgroup waits for C-finish work items: the finish is split so that nobody computes it alone:
+//   tail of iteration i (every tile): its dC slab rows and its tile sums of the scalar partials
+//     (canon_totals' tile level), stored write-through; an arrival ticket on the counter of its
+//     tile group g = t % 16; the group's LAST arrival (told by its ticket, no wait) sums the
+//     group's tiles in order -- the dC columns exactly as cfinish's virtual wave g does, the
+//     scalars at canon_totals' group level -- into the group record G[i & 1][g] (write-through)
+//     and counts the group complete on the top counter;
+//   head of iteration i+1 (every workgroup): one poll of the top counter until every group of
+//     iteration i is complete, then EVERY workgroup sums the 16 group records in g order and
+//     runs the C-step's regulariser + Adam (+ projection) itself -- cfinish's arithmetic on
+//     cfinish's operands in cfinish's order, so every workgroup holds the same new C bit for
+//     bit, straight into its LDS C^T -- and the state book-keeping of cfinish + the S-step's
+//     start (LoopState, workgroup 0 appends the history row).  The new moments mC, vC go to a
+//     ping-pong buffer written by workgroup 0 alone (read one iteration later).
+// Every value another workgroup reads is stored sc1 and loaded sc1 after a counter it polled or
+// a ticket it took, behind `s_waitcnt vmcnt(0)` + the workgroup barrier on the producer side
+// (MI355X_MICROARCH.md, hand-off forms: no release / acquire fence, whose L2 write-back would
+// drain the S-step's 25 MB of rows).  A wait past kLoopSpin polls sets the state's fault word
+// and every workgroup leaves.  After the loop workgroup 0 waits for the last groups (every
+// workgroup has then left its last head) and writes C, mC, vC and qsc_state as the launch pairs
+// would have left them before their last qsc_cfinish -- which the caller then issues, on the
+// slab of the last C-pass, followed by the closing qsc_spass (qmc.issue_iterations).
 // ---------------------------------------------------------------------------------------
-// scfused_tile, then each workgroup takes an arrival ticket (device-scope atomic on its tile
-// group's workspace counter, after its writes are complete device-wide, fin_arrive); the last
-// arrivals of each group, R*nks + 2 workgroups in all, wait until every tile has arrived and
-// then run the C-finish work items (cfinish_vb), the others leave.  The C-step finish that was
-// a launch of its own rides on the tail of the fused launch: same code, operands and order as
-// (qsc_scpass, qsc_cfinish mode 1), so the same results bit for bit, one launch per iteration
-// instead of two.  Co-residency: a waiting workgroup keeps its CU; at most R*nks + 2 wait, so
-// every other tile finds a CU as long as the device holds more workgroups than that -- the host
-// checks it against the kernel's occupancy times the CU count, with a margin for other streams
-// (qsc_scpass_fin_supported, fin_fits).  A wait past kFinSpin polls (other work holding the CUs
-// despite the check) sets the state's sticky fault word and skips the item.
-constexpr unsigned kFinSpin = 1u << 20;
-constexpr int kFinGroups = 8;                      // arrival-ticket groups (PassWs::sync)
-constexpr int kSyncDone = 16 * (kFinGroups + 1);   // PassWs::sync word: completed C-finish items
-constexpr int kSyncWords = 16 * (kFinGroups + 2);
-
-// One poll of a cross-workgroup counter (arrival tickets, completed C-finish items): a relaxed
-// agent-scope load (`global_load ... sc1`).  Polling with an atomic add of an opaque zero
-// instead (a literal zero is folded back into the load) was measured: no change for the fused
-// finish, 23.6 -> 33.5 us per persistent-loop iteration at C3 (256 workgroups polling one
-// line with atomics).
-__device__ __forceinline__ unsigned long long poll_ctr(unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Arrival of tile t at the fused finish (thread 0 of its workgroup, after its stores completed):
-// the tiles count in kFinGroups groups (t mod G) on counters of their own -- the atomics on one
-// counter are serialised, and at C2 the tiles of a launch arrive together (measured: tools/micro/
-// atomic_contention.hip) -- and the last arrival of a group counts the group complete.  The last
-// q_g arrivals of group g run the C-finish items g, g + G, ... (q_g of them; all R*nks + 2 over
-// the groups) once every group is complete.  Counters run for the life of the workspace: every
-// launch adds n_g to group g and G to the completed count (the same tile count every launch).
-// Returns the item (-1: none) or `timeout_vb` when the wait passed kFinSpin polls.
-__device__ __forceinline__ int fin_arrive(unsigned long long* sync, const int t, const int nt,
-                                          const int nvb, int* fault, const int timeout_vb) {
-  const int G = nt < kFinGroups ? nt : kFinGroups;
-  const int g = t % G;
-  const unsigned long long ng = (unsigned long long)((nt - g + G - 1) / G);
-  const unsigned long long qg = g < nvb ? (unsigned long long)((nvb - g + G - 1) / G) : 0ull;
-  const unsigned long long tk =
-      __hip_atomic_fetch_add(sync + 16 * g, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long a = tk % ng, launch = tk / ng;
-  unsigned long long* const groups = sync + 16 * kFinGroups;
-  if (a == ng - 1) __hip_atomic_fetch_add(groups, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (a + qg < ng) return -1;
-  const int vb = g + G * (int)(a + qg - ng);
-  const unsigned long long target = (launch + 1) * (unsigned long long)G;
-  unsigned polls = 0;
-  while (poll_ctr(groups) < target) {
-    if (++polls > kFinSpin) {
-      __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return timeout_vb;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  return vb;
-}
-
-template <int RP, typename E, int KIND, bool LOG>
-__global__ void __launch_bounds__(FusedBlock<RP>::v) scfin_kernel(
-    QSC_SCFIN_KPARAMS, float* __restrict__ mC, float* __restrict__ vC, qsc_adam adc,
-    float lambda_c, float* __restrict__ hist, int hist_cap, AdamCache* __restrict__ acache_c,
-    unsigned long long* sync) {
-  scfused_tile<RP, E, KIND, LOG, true>(QSC_SCF_ARGS, (int)blockIdx.x, (int)gridDim.x,
-                                       threadIdx.x);
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int nt = gridDim.x, nvb = R * nks + 2;
-  // C-finish scratch and the arrival broadcast word, over the (now idle) tile LDS
-  float(*red)[64] = reinterpret_cast<float(*)[64]>(smem);
-  float(*sh3)[kFWaves] = reinterpret_cast<float(*)[kFWaves]>(smem + kFWaves * 64);
-  Scalars& sc = *reinterpret_cast<Scalars*>(smem + kFWaves * 64 + 3 * kFWaves);
-  int* vbl = reinterpret_cast<int*>(smem + kFWaves * 64 + 3 * kFWaves + 16);
-  int* fault = reinterpret_cast<int*>(st) + 9;              // qsc_state.fused_fault
-  // Ordering, chosen for the 8 non-coherent XCD L2s: everything the C-finish items read was
-  // stored write-through at agent scope by the tile body (st_fin), so each wave waits for its
-  // own stores to complete (vmcnt 0: at the device coherence point), the workgroup barrier
-  // joins the waves, and thread 0 takes its arrival ticket with a relaxed agent-scope increment
-  // (fin_arrive; 64-bit counters: they count every workgroup of every launch for the life of the
-  // workspace and must stay aligned to launches, so they may never wrap) -- no release fence,
-  // whose L2 write-back per workgroup (while 25 MB of S-step writes stream through the L2s) cost
-  // ~6 us per launch.  Waiters poll with relaxed agent-scope loads (an acquire load per poll
-  // would invalidate this XCD's L2 under the workgroups still running there, measured 160 us per
-  // launch instead of ~34) and take no acquire fence: every value the C-finish item reads from
-  // this launch's other workgroups is loaded sc1 (ld_fin); C, mC, vC and the C-side Adam cache
-  // are from the previous launch.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-#if QSC_DIAG_STAMPS
-    g_stamps[(int)blockIdx.x * (FusedBlock<RP>::v / 64) * kStamps + 19] = __builtin_amdgcn_s_memtime();
-#endif
-    *vbl = fin_arrive(sync, (int)blockIdx.x, nt, nvb, fault, -1);
-  }
-  [[maybe_unused]] const int wg = (int)blockIdx.x * (FusedBlock<RP>::v / 64) + (threadIdx.x >> 6);
-  STAMP(wg, 20);  // (diagnostic builds) wave 0: ticket taken and, for a waiter, the wait over
-  __syncthreads();
-  const int vb = *vbl;
-  if (vb < 0) return;
-  cfinish_vb<true>(vb, red, sc, sh3, slab, nt, nks, R, K, C, 1, nullptr, mC, vC, adc, lambda_c,
-                   nullptr, cnsq, st, part_nll_c, nt * nks, part_nll_s, part_nsq_s,
-                   nt * PT / QSC_SLICE, hist, hist_cap, acache_c);
-  STAMP(wg, 21);  // C-finish item done
-}
-
-// ---------------------------------------------------------------------------------------
-// Persistent fused loop (qsc_scpass_loop): n fused bodies (S-step i + C-pass i+1 + that
-// C-step's finish) in ONE launch.  One workgroup per tile for the whole launch (every
-// workgroup co-resident: the host checks occupancy x CUs >= tiles).  Per iteration: the tile
-// body and the fused-finish tail of scfin_kernel, every cross-workgroup value stored write-
-// through at agent scope (st_fin, cfinish_vb<true>); each finishing workgroup then counts its
-// item in the state's fin_done word, and every workgroup waits for the iteration's R*nks + 2
-// items before the next tile body (one acquire fence: C, the state and the Adam cache were
-// written by other workgroups).  What a kernel boundary costs per iteration -- the drain, the
-// dispatch of 256 workgroups, kernel-argument reads, the cold start of every wave -- is gone;
-// S, mS and vS rows stay in the XCD's L2 between iterations (each tile reads back only its own
-// rows, written by the same wave).  The arguments are read every iteration from the kernarg segment
-// through an offset laundered by an empty asm, and so are the workgroup and thread indices:
-// nothing derived from them is hoisted out of the loop and kept live across it (a first
-// persistent attempt spilled 113 SGPRs keeping the arguments; as plain kernel arguments inside
-// a loop they are not rematerialised as in the one-shot kernels: 202 SGPR spills).  A wait past kFinSpin
-// polls sets fused_fault and every workgroup leaves the loop.
-constexpr int kLoopTimeout = -0x40000000;  // the ticket wait timed out (vb sentinel)
+constexpr unsigned kLoopSpin = 1u << 21;
+// PassWs::sync words, each counter on a 128-B line of its own (only atomics and sc1 loads touch
+// them), zeroed by the launcher before every loop launch: [16 g] group g's arrivals,
+// [16 kTGroups] completed groups
+constexpr int kSyncTop = 16 * kTGroups;
+constexpr int kSyncWords = 16 * (kTGroups + 1);
 
 struct LoopArgs {
   const void* s_ent;
@@ -2342,118 +2323,337 @@ struct LoopArgs {
   float* mC;
   float* vC;
   float* hist;
-  AdamCache* acache_c;
+  float* grec;   // [2][kTGroups][R Kp + 4] group records (dC columns, then nll_c, nll_s, nsq_s)
+  float* tsum;   // [ntiles][4] tile sums (nll_c, nll_s, nsq_s)
+  float* mvbuf;  // [2][2][R K] the moments mC, vC of the head, ping-pong
+  unsigned long long* sync;
   qsc_adam ad;
   qsc_adam adc;
   Lik lk;
   float lambda_s, lambda_c;
   int nks, NP, PT, nbins, R, K, hist_cap, n;
-  int* progress;  // nullable diagnostics: per workgroup, 16 * iteration + phase reached
-  unsigned long long* sync;  // PassWs::sync: group tickets, completed groups and C-finish items
+  size_t tile_lds;  // bytes of the tile body's LDS (the LoopState follows)
   Edges E;
 };
 using LoopKA = const char __attribute__((address_space(4)));
 #define QSC_LA(f) (*(const decltype(LoopArgs::f)*)(const char*)(kb + offsetof(LoopArgs, f)))
 
-// one iteration of scloop_kernel (kb, t and tidx laundered by the caller); false: leave the loop
-template <int RP, typename E, int KIND, bool LOG>
-__device__ __forceinline__ bool scloop_iter(LoopKA* kb, const int t, const unsigned tidx, int it,
-                                            int n, unsigned long long done0) {
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// sc1 buffer loads of a group of independent words (the relaxed atomic loads above are waited
+// one by one; these are batched like plain loads).  Byte offsets below 2^31.
+__device__ __forceinline__ float ld_sc1b(const float* base, int64_t idx) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base),
+                                                                     (short)0, 0x7fffffff,
+                                                                     0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b32(r, (int)(idx * 4), 0, 16);  // aux 16: sc1
+}
+
+// ||C||^2 of the LDS C^T as scfused_tile's t == 0 forms it (threads < 256 over flat indices
+// t, t + 256, ..., then block_sum): the value cfinish reads from the C-pass
+__device__ __forceinline__ float ct_norm_sq(const float* Cl, int CP, int R, int K, float* sh,
+                                            unsigned tidx) {
+  float s2 = 0.0f;
+  if (tidx < 256)
+    for (int i = (int)tidx; i < R * K; i += 256) {
+      const int r = i / K, k = i - r * K;
+      const float c = Cl[k * CP + r];
+      s2 = __builtin_fmaf(c, c, s2);
+    }
+  return block_sum_tid(s2, sh, tidx);
+}
+
+// the head of iteration it >= 1 (see above); false: a wait timed out (leave the loop)
+template <int RP, int KIND>
+__device__ bool loop_head(LoopKA* kb, const int t, const unsigned tidx, const int it,
+                          LoopState* ll, const int nG) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int nt = (int)gridDim.x;
-  qsc_state* st = QSC_LA(st);
-  const int R = QSC_LA(R), nks = QSC_LA(nks);
-  const Edges& E_ = *(const Edges*)(const char*)(kb + offsetof(LoopArgs, E));
-  int* const prog = QSC_LA(progress);
-  auto mark = [&](int phase) {
-    if (prog && tidx == 0)
-      __hip_atomic_store(prog + t, 16 * it + phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  mark(1);
-  scfused_tile<RP, E, KIND, LOG, true>(
-      reinterpret_cast<const E*>(QSC_LA(s_ent)), QSC_LA(s_width), QSC_LA(s_off),
-      reinterpret_cast<const E*>(QSC_LA(c_ent)), QSC_LA(c_width), QSC_LA(c_off), QSC_LA(c_kmap),
-      nks, QSC_LA(NP), QSC_LA(PT), QSC_LA(lk), E_, QSC_LA(nbins), R, QSC_LA(K), QSC_LA(S),
-      QSC_LA(C), QSC_LA(mS), QSC_LA(vS), QSC_LA(ad), QSC_LA(lambda_s), st, QSC_LA(part_nll_s),
-      QSC_LA(part_nsq_s), QSC_LA(slab), QSC_LA(part_nll_c), QSC_LA(cnsq), QSC_LA(acache),
-      nullptr, t, nt, tidx);
-  const int nvb = R * nks + 2;
-  float(*red)[64] = reinterpret_cast<float(*)[64]>(smem);
-  float(*sh3)[kFWaves] = reinterpret_cast<float(*)[kFWaves]>(smem + kFWaves * 64);
-  Scalars& sc = *reinterpret_cast<Scalars*>(smem + kFWaves * 64 + 3 * kFWaves);
-  int* vbl = reinterpret_cast<int*>(smem + kFWaves * 64 + 3 * kFWaves + 16);
-  unsigned long long* const sync = QSC_LA(sync);
-  unsigned long long* done = sync + kSyncDone;
-  int* fault = reinterpret_cast<int*>(st) + 9;
-  mark(2);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (st_fin stores complete: see scfin)
-  __syncthreads();
+  Scalars& sc = *reinterpret_cast<Scalars*>(smem);
+  float* Cl = smem + 8;
+  constexpr int CP = TP<RP, KIND>::v;
+  const int R = QSC_LA(R), K = QSC_LA(K), nks = QSC_LA(nks);
+  const int Kp = nks * 64, RK = R * K, gsz = R * Kp + 4;
+  unsigned long long* sync = QSC_LA(sync);
   if (tidx == 0) {
-    // >= 0: a C-finish item; -1: none; kLoopTimeout: timed out
-    const int vb = fin_arrive(sync, t, nt, nvb, fault, kLoopTimeout);
-    if (vb >= 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    *vbl = vb;
-  }
-  __syncthreads();
-  const int vb = *vbl;
-  mark(vb == kLoopTimeout ? 9 : 3);
-  if (vb == kLoopTimeout) return false;  // (timed out: leave; the others time out on fin_done)
-  if (vb >= 0) {
-    cfinish_vb<true>(vb, red, sc, sh3, QSC_LA(slab), nt, nks, R, QSC_LA(K), QSC_LA(C), 1,
-                     nullptr, QSC_LA(mC), QSC_LA(vC), QSC_LA(adc), QSC_LA(lambda_c), nullptr,
-                     QSC_LA(cnsq), st, QSC_LA(part_nll_c), nt * nks, QSC_LA(part_nll_s),
-                     QSC_LA(part_nsq_s), nt * QSC_LA(PT) / QSC_SLICE, QSC_LA(hist),
-                     QSC_LA(hist_cap), QSC_LA(acache_c));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tidx == 0)
-      __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    mark(4);
-  }
-  if (it + 1 >= n) return true;
-  // the next tile body reads C, the state and the Adam caches: wait for every C-finish item of
-  // this iteration, then one acquire fence
-  if (tidx == 0) {
-    const unsigned long long target = done0 + (unsigned long long)nvb * (unsigned long long)(it + 1);
     unsigned polls = 0;
-    int ok = 1;
-    while (poll_ctr(done) < target) {
-      if (++polls > kFinSpin) {
-        __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
+    while (__hip_atomic_load(sync + kSyncTop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+           (unsigned long long)nG * (unsigned long long)it) {
+      if (++polls > kLoopSpin) {
+        ll->fault = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    *vbl = ok;
   }
   __syncthreads();
-  const int ok = *vbl;
-  __syncthreads();  // (the LDS word is tile LDS again in the next body)
-  mark(ok ? 5 : 10);
-  return ok != 0;
+  if (ll->fault) return false;
+  const float* G = QSC_LA(grec) + (size_t)((it - 1) & 1) * kTGroups * gsz;
+  // ||C_i||^2 of the C the last C-pass used (the LDS C^T) and the C-step scalars
+  const float nsq_c = ct_norm_sq(Cl, CP, R, K, ll->sh, tidx);
+  if (tidx == 0) {
+    const float nrm = sqrtf(nsq_c);
+    ll->scc.coef = nrm > 0.0f ? QSC_LA(lambda_c) / nrm : 0.0f;
+    ll->scc.as = ll->as_c;
+  }
+  __syncthreads();
+  // the C-step: per (r, k) the 16 group sums in g order (cfinish's red[0..15]), + coef C, Adam
+  const qsc_adam adc = QSC_LA(adc);
+  const float coef = ll->scc.coef;
+  const AdamScalars asc = ll->scc.as;
+  const float* mvin = it == 1 ? nullptr : QSC_LA(mvbuf) + (size_t)((it - 1) & 1) * 2 * RK;
+  float* mvout = QSC_LA(mvbuf) + (size_t)(it & 1) * 2 * RK;
+  const float* mC = QSC_LA(mC);
+  const float* vC = QSC_LA(vC);
+  const int Ko = sr_off(K);
+  constexpr int kCols = 2;  // columns per pass per thread (16 group loads each in flight)
+  for (int b0 = 0; b0 < RK; b0 += kCols * (int)blockDim.x) {  // (uniform trip count: barrier)
+    const int i0 = b0 + (int)tidx;
+    float gv[kCols][kTGroups];
+    float m[kCols], v[kCols], p[kCols];
+#pragma unroll
+    for (int c = 0; c < kCols; ++c) {
+      const int i = min(i0 + c * (int)blockDim.x, RK - 1);
+      const int r = i / K, k = i - r * K;
+      const int col = r * Kp + k;
+#pragma unroll
+      for (int g = 0; g < kTGroups; ++g) gv[c][g] = ld_sc1b(G, (int64_t)g * gsz + col);
+      m[c] = mvin ? ld_sc1b(mvin, i) : mC[i];
+      v[c] = mvin ? ld_sc1b(mvin, RK + i) : vC[i];
+      p[c] = Cl[k * CP + r];
+    }
+#pragma unroll
+    for (int c = 0; c < kCols; ++c) {
+      float g = gv[c][0];
+#pragma unroll
+      for (int gg = 1; gg < kTGroups; ++gg) g += gv[c][gg];
+      g = __fadd_rn(g, __fmul_rn(p[c], coef));
+      adam_elem(p[c], m[c], v[c], g, adc, asc);
+    }
+    __syncthreads();  // every thread has read its old C^T entries of this pass
+#pragma unroll
+    for (int c = 0; c < kCols; ++c) {
+      const int i = i0 + c * (int)blockDim.x;
+      if (i >= RK) continue;
+      const int r = i / K, k = i - r * K;
+      Cl[k * CP + r] = p[c];
+      if constexpr (is_sr(KIND)) Cl[(Ko + k) * CP + r] = -p[c];
+      if (t == 0) {
+        __hip_atomic_store(mvout + i, m[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(mvout + RK + i, v[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  if (tidx == 0) {
+    // cfinish's book-keeping block (the settle of the last S-step, the C-pass NLL), then the
+    // S-step's start (scfused_tile, t == 0), on the group records' scalars summed in g order
+    float sv[3][kTGroups];
+#pragma unroll
+    for (int g = 0; g < kTGroups; ++g)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) sv[j][g] = ld_sc1b(G, (int64_t)g * gsz + R * Kp + j);
+    float nll_c = 0.0f, nll_s = 0.0f, nsq_s = 0.0f;
+#pragma unroll
+    for (int g = 0; g < kTGroups; ++g) {
+      nll_c += sv[0][g];
+      nll_s += sv[1][g];
+      nsq_s += sv[2][g];
+    }
+    int pend = ll->pending;
+    if (pend & (QSC_PEND_SNLL | QSC_PEND_SUPD)) {
+      const int hi = ll->iter - 1;
+      float* hist = QSC_LA(hist);
+      if (t == 0 && hist && hi >= 0 && hi < QSC_LA(hist_cap)) {
+        hist[4 * hi + 0] = ll->nll_c;
+        hist[4 * hi + 1] = nll_s;
+        hist[4 * hi + 2] = ll->normsq_c;
+        hist[4 * hi + 3] = ll->normsq_s_prev;
+      }
+      ll->nll_s = nll_s;
+      if (pend & QSC_PEND_SUPD) {
+        ll->normsq_s = nsq_s;
+        ll->step_s += 1;
+      }
+      pend &= ~(QSC_PEND_SNLL | QSC_PEND_SUPD);
+    }
+    ll->nll_c = nll_c;
+    ll->normsq_c = nsq_c;
+    pend |= QSC_PEND_C;
+    // the S-step's start
+    ll->step_c += 1;  // (the C update of this head)
+    pend = (pend & ~QSC_PEND_C) | QSC_PEND_SNLL | QSC_PEND_SUPD;
+    ll->pending = pend;
+    ll->normsq_s_prev = ll->normsq_s;
+    ll->iter += 1;
+    const float nrm = sqrtf(ll->normsq_s);
+    sc.coef = nrm > 0.0f ? QSC_LA(lambda_s) / nrm : 0.0f;
+    sc.as = ll->as_s;
+  }
+  __syncthreads();
+  return true;
+}
+
+// the tail of iteration it: tile sums, arrival ticket, the group record by the last arrival;
+// and (off the critical path, wave 1) the next iteration's Adam scalars
+template <int RP>
+__device__ void loop_tail(LoopKA* kb, const int t, const int nt, const unsigned tidx,
+                          const int it, LoopState* ll, const int nG) {
+  const int R = QSC_LA(R), nks = QSC_LA(nks), Kp = nks * 64, gsz = R * Kp + 4;
+  const int nsl = QSC_LA(PT) / QSC_SLICE;
+  unsigned long long* sync = QSC_LA(sync);
+  float* tsum = QSC_LA(tsum);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab / partial stores
+  __syncthreads();  // (and the LoopState partials of every wave)
+  const int g = t % kTGroups;
+  if (tidx == 0) {
+    // canon_totals' tile level: the tile's items in order
+    float a = 0.0f, b = 0.0f, c = 0.0f;
+    for (int l = 0; l < nsl; ++l) {
+      a += ll->ts[l];
+      b += ll->ts[nsl + l];
+    }
+    for (int ks = 0; ks < nks; ++ks) c += ll->ts[2 * nsl + ks];
+    __hip_atomic_store(tsum + 4 * t + 0, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(tsum + 4 * t + 1, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(tsum + 4 * t + 2, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long ng = (unsigned long long)((nt - g + kTGroups - 1) / kTGroups);
+    const unsigned long long v =
+        __hip_atomic_fetch_add(sync + 16 * g, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ll->last = ((v + 1) % ng) == 0;
+  }
+  if (tidx == 64 && it + 1 < QSC_LA(n)) {
+    // the next head's C-step and next S-step Adam scalars (the double-precision bias
+    // corrections: ~1 us on one lane, here while the group is being reduced)
+    ll->as_c = adam_scalars(QSC_LA(adc), ll->step_c + 1);
+    ll->as_s = adam_scalars(QSC_LA(ad), ll->step_s + 2);
+  }
+  __syncthreads();
+  if (!ll->last) return;
+  // the group record: cfinish's virtual wave g on every dC column, canon_totals' group level
+  const float* slab = QSC_LA(slab);
+  float* rec = QSC_LA(grec) + (size_t)(it & 1) * kTGroups * gsz + (size_t)g * gsz;
+  const int ncol = R * Kp;
+  for (int col = tidx; col < ncol; col += blockDim.x) {
+    float v[16];
+    float acc = 0.0f;
+    for (int j0 = g; j0 < nt; j0 += 16 * kTGroups) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int tt = min(j0 + j * kTGroups, nt - 1);
+        v[j] = ld_sc1b(slab, (int64_t)tt * ncol + col);
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (j0 + j * kTGroups < nt) acc += v[j];
+    }
+    __hip_atomic_store(rec + col, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tidx < 3) {
+    float acc = 0.0f;
+    for (int j0 = g; j0 < nt; j0 += 16 * kTGroups) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        v[j] = ld_sc1b(tsum, 4 * (int64_t)min(j0 + j * kTGroups, nt - 1) + tidx);
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (j0 + j * kTGroups < nt) acc += v[j];
+    }
+    __hip_atomic_store(rec + ncol + tidx, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tidx == 0)
+    __hip_atomic_fetch_add(sync + kSyncTop, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  (void)nG;
 }
 
 template <int RP, typename E, int KIND, bool LOG>
 __global__ void __launch_bounds__(FusedBlock<RP>::v) scloop_kernel(LoopArgs args) {
   LoopKA* const kp = (LoopKA*)__builtin_amdgcn_kernarg_segment_ptr();
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   int n = 0;
-  unsigned long long done0 = 0;
   {
     LoopKA* const kb = kp;
     n = QSC_LA(n);
-    // the fin_done base: every finish of this launch completes after every workgroup has taken
-    // its first ticket, i.e. after this read (thread 0 keeps it)
-    if (threadIdx.x == 0)
-      done0 = __hip_atomic_load(QSC_LA(sync) + kSyncDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   (void)args;
   for (int it = 0; it < n; ++it) {
     int o = 0, t = (int)blockIdx.x;
     unsigned tidx = threadIdx.x;
     asm volatile("" : "+s"(o), "+s"(t), "+v"(tidx));  // re-derived every iteration
-    if (!scloop_iter<RP, E, KIND, LOG>(kp + o, t, tidx, it, n, done0)) return;
+    LoopKA* const kb = kp + o;
+    const int nt = (int)gridDim.x, nG = nt < kTGroups ? nt : kTGroups;
+    LoopState* ll = reinterpret_cast<LoopState*>(reinterpret_cast<char*>(smem) + QSC_LA(tile_lds));
+    if (it > 0 && !loop_head<RP, KIND>(kb, t, tidx, it, ll, nG)) break;
+    scfused_tile<RP, E, KIND, LOG, true, true>(
+        reinterpret_cast<const E*>(QSC_LA(s_ent)), QSC_LA(s_width), QSC_LA(s_off),
+        reinterpret_cast<const E*>(QSC_LA(c_ent)), QSC_LA(c_width), QSC_LA(c_off),
+        QSC_LA(c_kmap), QSC_LA(nks), QSC_LA(NP), QSC_LA(PT), QSC_LA(lk),
+        *(const Edges*)(const char*)(kb + offsetof(LoopArgs, E)), QSC_LA(nbins), QSC_LA(R),
+        QSC_LA(K), QSC_LA(S), QSC_LA(C), QSC_LA(mS), QSC_LA(vS), QSC_LA(ad), QSC_LA(lambda_s),
+        QSC_LA(st), QSC_LA(part_nll_s), QSC_LA(part_nsq_s), QSC_LA(slab), QSC_LA(part_nll_c),
+        QSC_LA(cnsq), QSC_LA(acache), nullptr, t, nt, tidx, it > 0, ll);
+    loop_tail<RP>(kb, t, nt, tidx, it, ll, nG);
+  }
+  // workgroup 0: once every group of the last iteration is complete (every workgroup has left
+  // its last head), the state, C and its moments as the launch pairs leave them before their
+  // last qsc_cfinish; the fault word
+  int o = 0, t = (int)blockIdx.x;
+  unsigned tidx = threadIdx.x;
+  asm volatile("" : "+s"(o), "+s"(t), "+v"(tidx));
+  LoopKA* const kb = kp + o;
+  LoopState* ll = reinterpret_cast<LoopState*>(reinterpret_cast<char*>(smem) + QSC_LA(tile_lds));
+  qsc_state* st = QSC_LA(st);
+  if (t != 0) {
+    if (tidx == 0 && ll->fault)
+      __hip_atomic_store(&st->fused_fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const int nt = (int)gridDim.x, nG = nt < kTGroups ? nt : kTGroups;
+  unsigned long long* sync = QSC_LA(sync);
+  if (tidx == 0 && !ll->fault) {
+    unsigned polls = 0;
+    while (__hip_atomic_load(sync + kSyncTop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+           (unsigned long long)nG * (unsigned long long)n) {
+      if (++polls > kLoopSpin) {
+        ll->fault = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  if (ll->fault) {
+    if (tidx == 0) __hip_atomic_store(&st->fused_fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const int R = QSC_LA(R), K = QSC_LA(K), RK = R * K;
+  constexpr int CP = TP<RP, KIND>::v;
+  const float* Cl = smem + 8;
+  float* C = QSC_LA(C);
+  float* mC = QSC_LA(mC);
+  float* vC = QSC_LA(vC);
+  if (n >= 2) {  // (n == 1: C, mC, vC are those the loop started from)
+    const float* mv = QSC_LA(mvbuf) + (size_t)((n - 1) & 1) * 2 * RK;
+    for (int i = tidx; i < RK; i += blockDim.x) {
+      const int r = i / K, k = i - r * K;
+      C[i] = Cl[k * CP + r];
+      mC[i] = ld_sc1(mv + i);
+      vC[i] = ld_sc1(mv + RK + i);
+    }
+  }
+  if (tidx == 0) {
+    st->step_s = ll->step_s;
+    st->step_c = ll->step_c;
+    st->iter = ll->iter;
+    st->pending = ll->pending;
+    st->normsq_s = ll->normsq_s;
+    st->normsq_c = ll->normsq_c;
+    st->nll_c = ll->nll_c;
+    st->nll_s = ll->nll_s;
+    st->normsq_s_prev = ll->normsq_s_prev;
   }
 }
 #undef QSC_LA
@@ -2496,10 +2696,11 @@ __global__ void __launch_bounds__(kFBlock) cupdate_kernel(
 __global__ void __launch_bounds__(1024) flush_kernel(qsc_state* __restrict__ st,
                                                      const float* __restrict__ part_nll_s,
                                                      const float* __restrict__ part_nsq_s,
-                                                     int nslices, float* __restrict__ hist,
-                                                     int hist_cap) {
-  __shared__ float sh[16];
-  settle_s(st, part_nll_s, part_nsq_s, nslices, hist, hist_cap, sh);
+                                                     int ntiles, int nslices,
+                                                     float* __restrict__ hist, int hist_cap) {
+  __shared__ float ts[3 * 1024];
+  __shared__ float gs[3 * kTGroups];
+  settle_s(st, part_nll_s, part_nsq_s, ntiles, nslices / ntiles, hist, hist_cap, ts, gs);
   if (threadIdx.x == 0 && (st->pending & QSC_PEND_C)) {
     st->step_c += 1;
     st->pending &= ~QSC_PEND_C;
@@ -2646,17 +2847,20 @@ struct PassWs {
   int* sched;       // S-pass queue counters [kSchedQ] + finished-wave counter (zero between launches)
   float* cnsq;      // ||C||^2 of the C the last C-pass read (written by the C-pass)
   AdamCache* acache;  // [0..1] S-side, [2..3] C-side step scalars (adam_scalars_cached)
-  // cross-workgroup counters of the fused-finish launches, each on a 128-B line of its own that
-  // only atomics and agent-scope (sc1) loads touch: [16 g] the arrival tickets of tile group g
-  // (g < kFinGroups), [16 kFinGroups] completed groups, [16 (kFinGroups + 1)] the persistent
-  // loop's completed C-finish items.  An sc1 load is served by the XCD's L2, so a counter on a
-  // line that plain loads also bring into an L2 (the state's other fields) can be read stale
-  // there for as long as the line stays (seen: a persistent-loop wait that never ended).
-  // Zero-filled with the workspace; they only ever count up.
+  // the persistent loop's cross-workgroup counters (kSyncWords), each on a 128-B line of its own
+  // that only atomics and agent-scope (sc1) loads touch -- an sc1 load is served by the XCD's
+  // L2, so a counter on a line that plain loads also bring into an L2 can be read stale there
+  // (seen in round 4: a wait that never ended); zeroed by the loop's launcher
   unsigned long long* sync;
+  float* grec;   // [2][kTGroups][R Kp + 4] the loop's group records
+  float* tsum;   // [ntiles][4] the loop's tile sums
+  float* mvbuf;  // [2][2][R K] the loop's C-side moments, ping-pong
 };
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+inline size_t grec_bytes(const qsc_obs_desc* d, int R) {
+  return (size_t)2 * kTGroups * ((size_t)R * d->nks * 64 + 4) * 4;
+}
 
 PassWs carve(const qsc_obs_desc* d, int R, void* ws) {
   char* w = (char*)ws;
@@ -2679,6 +2883,12 @@ PassWs carve(const qsc_obs_desc* d, int R, void* ws) {
   p.acache = (AdamCache*)w;
   w += al(4 * sizeof(AdamCache));
   p.sync = (unsigned long long*)w;
+  w += al(kSyncWords * sizeof(unsigned long long));
+  p.grec = (float*)w;
+  w += al(grec_bytes(d, R));
+  p.tsum = (float*)w;
+  w += al((size_t)d->ntiles * 4 * 4);
+  p.mvbuf = (float*)w;
   return p;
 }
 
@@ -2686,7 +2896,8 @@ size_t ws_bytes_for(const qsc_obs_desc* d, int R) {
   const int64_t Kp = (int64_t)d->nks * 64;
   return al((size_t)d->ntiles * R * Kp * 4) + al((size_t)d->ntiles * d->nks * 4) +
          2 * al((size_t)(d->Pp / QSC_SLICE) * 4) + al(256 * 8) + al((kSchedQ + 1) * 4) + al(4) +
-         al(4 * sizeof(AdamCache)) + al(kSyncWords * sizeof(unsigned long long));
+         al(4 * sizeof(AdamCache)) + al(kSyncWords * sizeof(unsigned long long)) +
+         al(grec_bytes(d, R)) + al((size_t)d->ntiles * 4 * 4) + al((size_t)4 * R * d->K * 4);
 }
 
 bool desc_ok(const qsc_obs_desc* d) {
@@ -3069,108 +3280,25 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
   return QSC_OK;
 }
 
-// CUs left to other streams (RCCL kernels, copies) when the fused-finish launch's late
-// workgroups must be co-resident
-constexpr int kFinCuMargin = 16;
-
-// the fused-finish launch's R*nks + 2 late workgroups fit on the device together: blocks per CU
-// of the exact kernel instance at its LDS size (cached per device, kernel and LDS size)
-static bool fin_fits(const void* kp, unsigned threads, size_t shm, int nvb) {
-  struct Key { int dev; const void* k; size_t shm; int cap; };
-  static Key cache[32];
-  static int ncache = 0;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  int cap = -1;
-  for (int i = 0; i < ncache; ++i)
-    if (cache[i].dev == dev && cache[i].k == kp && cache[i].shm == shm) cap = cache[i].cap;
-  if (cap < 0) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kp, (int)threads, shm) != hipSuccess)
-      nb = 0;
-    cap = nb * cu_count();
-    if (ncache < 32) cache[ncache++] = Key{dev, kp, shm, cap};
-  }
-  return nvb + kFinCuMargin <= cap;
-}
-
-QSC_API int qsc_scpass_fin_supported(const qsc_obs_desc* d, int32_t R) {
-  if (!qsc_scpass_supported(d, R)) return 0;
-  const int nvb = R * d->nks + 2;
-  // the C-finish work items run on the fused launch's 4..16-wave workgroups (cfinish_vb's
-  // virtual waves), one item per late arrival; the late arrivals must be co-resident (at least
-  // one workgroup per CU; the launch itself checks the kernel instance's exact occupancy).
-  // Ranks up to 8 (the instances built with the finish tail).
-  return (rp_of(R) <= 8 && scpass_threads(d, R) >= 256u && d->ntiles >= nvb &&
-          nvb + kFinCuMargin <= cu_count())
-             ? 1
-             : 0;
-}
-
-QSC_API int qsc_scpass_fin(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
-                           const int64_t* s_off, const void* c_entries, const int32_t* c_width,
-                           const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
-                           int32_t R, float* S, float* C, float* mS, float* vS,
-                           const qsc_adam* adam_s, float lambda_s, float* mC, float* vC,
-                           const qsc_adam* adam_c, float lambda_c, qsc_state* st, float* hist,
-                           int32_t hist_cap, void* ws, size_t ws_bytes, void* stream) {
-  if (!qsc_scpass_fin_supported(d, R) || !m || m->nbounds - 1 != d->nbins || !S || !C || !mS ||
-      !vS || !adam_s || !mC || !vC || !adam_c || !st || !s_width || !s_off || !c_width ||
-      !c_off || !c_kmap || (d->s_entries > 0 && !s_entries) ||
-      (d->c_entries > 0 && !c_entries) || !ws || ws_bytes < ws_bytes_for(d, R) ||
-      (hist_cap > 0 && !hist))
-    return QSC_EINVAL;
-  const int RP = rp_of(R);
-  const int kind = lik_kind(m);
-  const bool sr = d->rowfmt == 1;
-  if (!rowfmt_ok(d, R, kind)) return QSC_EINVAL;
-  const int NP = cpass_parts(d, R, sr);
-  const size_t shm = scfused_lds(d->PT, R, d->K, d->nks, NP, sr);
-  PassWs w = carve(d, R, ws);
-  Edges E;
-  make_edges(m, &E);
-  Lik lk = make_lik(m);
-  set_dbg(lk, d, sr);
-  if (kind == LIK_SQUARED)
-    make_sq_targets(m, &E);
-  else if (!m->log_model)
-    scale_edges(&E, m->nbounds - 1, lk.a);
-  const qsc_adam ad = *adam_s, adc = *adam_c;
-  const unsigned threads = scpass_threads(d, R);
-  (void)RP;
-  hipStream_t s = STREAM(stream);
-#define SCFIN_LAUNCH(RPV, ET, KD, LG)                                                          \
-  do {                                                                                         \
-    if constexpr (RPV <= 8) {                                                                  \
-      if (!fin_fits(reinterpret_cast<const void*>(scfin_kernel<RPV, ET, KD, LG>), threads, shm, \
-                    R * d->nks + 2))                                                           \
-        return QSC_EUNSUPPORTED;                                                               \
-      hipLaunchKernelGGL((scfin_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles),           \
-                         dim3(threads), shm, s, (const ET*)s_entries, s_width, s_off,          \
-                         (const ET*)c_entries, c_width, c_off, c_kmap, d->nks, NP, d->PT, lk,  \
-                         E, d->nbins, R, d->K, S, C, mS, vS, ad, lambda_s, st, w.snll, w.snsq, \
-                         w.slab, w.cnll, w.cnsq, w.acache, (const int*)nullptr, mC, vC,        \
-                         adc, lambda_c, hist, hist_cap, w.acache + 2, w.sync);                 \
-    } else {                                                                                   \
-      return QSC_EUNSUPPORTED;                                                                 \
-    }                                                                                          \
-  } while (0)
-  QSC_DISPATCH_PASS(SCFIN_LAUNCH);
-#undef SCFIN_LAUNCH
-  QSC_CHECK_LAUNCH();
-  return QSC_OK;
-}
-
 // every workgroup of the persistent loop resident at once: tiles <= blocks per CU x CUs
 static bool loop_fits(const void* kp, unsigned threads, size_t shm, int ntiles) {
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kp, (int)threads, shm) != hipSuccess)
     return false;
-  return ntiles <= nb * cu_count();
+  return nb >= 1 && ntiles <= nb * cu_count();
+}
+
+// the loop's LDS: the fused launch's, 16-B aligned, then its LoopState
+static size_t loop_shm(const qsc_obs_desc* d, int R, bool sr, size_t* tile) {
+  const int NP = cpass_parts(d, R, sr);
+  *tile = (scfused_lds(d->PT, R, d->K, d->nks, NP, sr) + 15) & ~(size_t)15;
+  return *tile + loop_lds(d->PT / QSC_SLICE, d->nks);
 }
 
 QSC_API int qsc_scpass_loop_supported(const qsc_obs_desc* d, int32_t R) {
-  if (!qsc_scpass_fin_supported(d, R)) return 0;
+  if (!qsc_scpass_supported(d, R) || rp_of(R) > 8) return 0;
+  size_t tile = 0;
+  if (loop_shm(d, R, d->rowfmt == 1, &tile) > 160 * 1024) return 0;
   return d->ntiles <= cu_count() ? 1 : 0;  // at most one workgroup per CU
 }
 
@@ -3182,20 +3310,6 @@ QSC_API int qsc_scpass_loop(const qsc_obs_desc* d, const void* s_entries, const 
                             const qsc_adam* adam_c, float lambda_c, qsc_state* st, float* hist,
                             int32_t hist_cap, int32_t n_iter, void* ws, size_t ws_bytes,
                             void* stream) {
-  return qsc_scpass_loop_dbg(d, s_entries, s_width, s_off, c_entries, c_width, c_off, c_kmap, m,
-                             R, S, C, mS, vS, adam_s, lambda_s, mC, vC, adam_c, lambda_c, st,
-                             hist, hist_cap, n_iter, nullptr, ws, ws_bytes, stream);
-}
-
-QSC_API int qsc_scpass_loop_dbg(const qsc_obs_desc* d, const void* s_entries,
-                                const int32_t* s_width, const int64_t* s_off,
-                                const void* c_entries, const int32_t* c_width,
-                                const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
-                                int32_t R, float* S, float* C, float* mS, float* vS,
-                                const qsc_adam* adam_s, float lambda_s, float* mC, float* vC,
-                                const qsc_adam* adam_c, float lambda_c, qsc_state* st,
-                                float* hist, int32_t hist_cap, int32_t n_iter, int32_t* progress,
-                                void* ws, size_t ws_bytes, void* stream) {
   if (!qsc_scpass_loop_supported(d, R) || !m || m->nbounds - 1 != d->nbins || !S || !C || !mS ||
       !vS || !adam_s || !mC || !vC || !adam_c || !st || !s_width || !s_off || !c_width ||
       !c_off || !c_kmap || (d->s_entries > 0 && !s_entries) ||
@@ -3206,9 +3320,9 @@ QSC_API int qsc_scpass_loop_dbg(const qsc_obs_desc* d, const void* s_entries,
   const int kind = lik_kind(m);
   const bool sr = d->rowfmt == 1;
   if (!rowfmt_ok(d, R, kind)) return QSC_EINVAL;
-  const int RP = rp_of(R);
   const int NP = cpass_parts(d, R, sr);
-  const size_t shm = scfused_lds(d->PT, R, d->K, d->nks, NP, sr);
+  size_t tile_lds = 0;
+  const size_t shm = loop_shm(d, R, sr, &tile_lds);
   PassWs w = carve(d, R, ws);
   LoopArgs la{};
   make_edges(m, &la.E);
@@ -3239,7 +3353,10 @@ QSC_API int qsc_scpass_loop_dbg(const qsc_obs_desc* d, const void* s_entries,
   la.mC = mC;
   la.vC = vC;
   la.hist = hist;
-  la.acache_c = w.acache + 2;
+  la.grec = w.grec;
+  la.tsum = w.tsum;
+  la.mvbuf = w.mvbuf;
+  la.sync = w.sync;
   la.ad = *adam_s;
   la.adc = *adam_c;
   la.lambda_s = lambda_s;
@@ -3252,11 +3369,14 @@ QSC_API int qsc_scpass_loop_dbg(const qsc_obs_desc* d, const void* s_entries,
   la.K = d->K;
   la.hist_cap = hist_cap;
   la.n = n_iter;
-  la.progress = progress;
-  la.sync = w.sync;
+  la.tile_lds = tile_lds;
   const unsigned threads = scpass_threads(d, R);
-  (void)RP;
+  const int RP = rp_of(R);
   hipStream_t s = STREAM(stream);
+  // counters from zero, group records zero (tile groups beyond the tile count stay empty)
+  if (hipMemsetAsync(w.sync, 0, kSyncWords * sizeof(unsigned long long), s) != hipSuccess ||
+      hipMemsetAsync(w.grec, 0, grec_bytes(d, R), s) != hipSuccess)
+    return QSC_EINVAL;
 #define SCLOOP_LAUNCH(RPV, ET, KD, LG)                                                         \
   do {                                                                                         \
     if constexpr (RPV <= 8) {                                                                  \
@@ -3312,7 +3432,7 @@ QSC_API int qsc_state_flush(const qsc_obs_desc* d, int32_t R, qsc_state* st, flo
     return QSC_EINVAL;
   PassWs w = carve(d, R, ws);
   hipLaunchKernelGGL(flush_kernel, dim3(1), dim3(1024), 0, STREAM(stream), st, w.snll, w.snsq,
-                     d->Pp / QSC_SLICE, hist, hist_cap);
+                     d->ntiles, d->Pp / QSC_SLICE, hist, hist_cap);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }

@@ -38,7 +38,7 @@ class SolveResult:
     Z: Optional[torch.Tensor] = None
     iters: int = 0
     fused: bool = False                 # S-step + next C-pass ran as one launch (qsc_scpass)
-    fin: bool = False                   # ... with the C-step finish in the same launch
+    loop: bool = False                  # ... all in one persistent launch (qsc_scpass_loop)
 
 
 # Longest run captured as one hipGraph; longer runs replay several (results are identical:
@@ -227,7 +227,7 @@ class FreeSSolver:
 
     def __init__(self, obs, S_init, C_init, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
                  betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024, fuse=True,
-                 T_true=None, nmse_every=0, fin=None, project_s=False, loop=None):
+                 T_true=None, nmse_every=0, project_s=False, loop=None):
         self.obs = obs
         R = S_init.shape[0]
         self.R = R
@@ -256,24 +256,15 @@ class FreeSSolver:
                                           dtype=torch.float64, device=self.S.device)
             self._nmse_ws = torch.empty(_lib.lib().qsc_reduce_workspace_bytes(0),
                                         dtype=torch.uint8, device=self.S.device)
-        # the fused body's C-step finish on the tail of its own launch (qsc_scpass_fin: one
-        # launch per iteration, bit-exact with the launch pair); not with per-iteration NMSE
-        # tracking, which runs between the S-step and that finish.  fin=None: off unless QSC_FIN=1
-        # (measured on MI355X at C3: 40.3 us for the one launch against 30.6 + 3.2 us for the
-        # launch pair, profiles/r04); fin=True/False forces it on/off where supported
-        if fin is None:
-            fin = os.environ.get("QSC_FIN", "0") == "1"
-        self.fin = (self.fuse and bool(fin) and not self.nmse_every
-                    and self.engine.scpass_fin_supported())
         # the fused bodies of a run in ONE persistent launch (qsc_scpass_loop: every tile's
-        # workgroup resident, a device-wide wait for the C-finish between bodies); opt-in with
-        # loop=True / QSC_LOOP=1 where supported, implies the fused finish
+        # workgroup resident, the C-step finish split over the tile groups and every
+        # workgroup's head; bit-exact with the launch pairs); not with per-iteration NMSE
+        # tracking, which runs between an S-step and the next finish.  loop=None: QSC_LOOP
+        # (default on); loop=True/False forces it on/off where supported
         if loop is None:
-            loop = os.environ.get("QSC_LOOP", "0") == "1"
+            loop = os.environ.get("QSC_LOOP", "1") == "1"
         self.loop = (self.fuse and bool(loop) and not self.nmse_every
                      and self.engine.scpass_loop_supported())
-        if self.loop:
-            self.fin = True
 
     # one outer iteration = C grad-step + S grad-step
     def c_step(self):
@@ -291,21 +282,19 @@ class FreeSSolver:
         self.s_step()
 
     def fused_body(self):
-        """S-step i fused with C-pass i+1, then C-step i+1's finish (needs a C-step before);
-        with `fin` all three in one launch."""
+        """S-step i fused with C-pass i+1, then C-step i+1's finish (needs a C-step before)."""
         e = self.engine
-        if self.fin:
-            e.scpass_fin(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s, self.mC,
-                         self.vC, self.adam_c, self.lambda_c)
-            return
         e.scpass(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s)
         self._track()  # (S_{i+1}, C_{i+1}): C is updated by the cfinish below
         e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)
 
     def fused_loop(self, n):
-        """n fused bodies (fused_body with `fin`, bit for bit) in one persistent launch."""
-        self.engine.scpass_loop(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s,
-                                self.mC, self.vC, self.adam_c, self.lambda_c, n)
+        """n fused bodies (fused_body x n, bit for bit) as one persistent launch and the last
+        body's C-step finish (qsc_scpass_loop, then qsc_cfinish)."""
+        e = self.engine
+        e.scpass_loop(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s, self.mC,
+                      self.vC, self.adam_c, self.lambda_c, n)
+        e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)
 
     def _track(self):
         if not self.nmse_every:
@@ -335,8 +324,8 @@ class FreeSSolver:
         prepare_iterations(self, n)
 
     def run(self, n, use_graph=False):
-        """Enqueue n outer iterations (no host sync).  With `fin`, read results through
-        S_pixels() / history() or call check(): they raise if a fused-finish wait timed out."""
+        """Enqueue n outer iterations (no host sync).  With `loop`, read results through
+        S_pixels() / history() or call check(): they raise if a persistent-loop wait timed out."""
         run_iterations(self, n, use_graph)
 
     # ---- results --------------------------------------------------------------------------
@@ -344,16 +333,16 @@ class FreeSSolver:
         return self.engine.read_state()
 
     def S_pixels(self):
-        if self.fin:
-            self.check()  # one small readback: a timed-out C-finish wait leaves C incomplete
+        if self.loop:
+            self.check()  # one small readback: a timed-out loop wait leaves C incomplete
         return self.obs.to_pixels(self.S, self.R).reshape(self.R, 1, self.obs.I, self.obs.J)
 
     def check(self):
-        """Raise if a fused-finish launch of this solver timed out waiting for the other tiles
-        (the run's C updates are then incomplete, include/qsc.h qsc_scpass_fin)."""
+        """Raise if a persistent-loop launch of this solver timed out waiting for the other
+        tiles (the run's C updates are then incomplete, include/qsc.h qsc_scpass_loop)."""
         if self.state().get("fused_fault"):
-            raise _lib.QscError("qsc_scpass_fin: the C-finish wait timed out; rerun with "
-                                "fin=False / QSC_FIN=0")
+            raise _lib.QscError("qsc_scpass_loop: a wait timed out; rerun with loop=False / "
+                                "QSC_LOOP=0")
 
     def history(self):
         self.engine.flush()  # settle the last S-pass (its history row)
@@ -376,7 +365,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
           betas=(0.9, 0.999), eps=1e-8, project_c=True, generator=None, Z_init=None,
           restart=False, restart_samples=(200, 200), T_true=None, nmse_every=0,
           use_graph=False, obs=None, tile=None, callback=None, loss="probit", fuse=True,
-          fin=None, project_s=False):
+          loop=None, project_s=False):
     """Alternating S/C probit-MLE (qmc/qmc.ipynb :559-645).
 
     Args mirror the notebook globals: Y (K,1,I,J) bin indices, Wx (K,1,I,J) 0/1 mask,
@@ -413,7 +402,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
         sol = FreeSSolver(obs, S_init, C_init, lambda_c, lambda_s, lr_c, lr_s, betas, eps,
                           project_c, hist_cap=max_iter, fuse=fuse,
                           T_true=T_true if nmse_every else None, nmse_every=nmse_every,
-                          fin=fin, project_s=project_s)
+                          loop=loop, project_s=project_s)
         done = 0
         chunk = nmse_every if (callback is not None and nmse_every) else max_iter
         while done < max_iter:
@@ -426,7 +415,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
         costs_c, costs_s = sol.history()
         return SolveResult(S=sol.S_pixels(), C=sol.C.clone(), costs_c=costs_c, costs_s=costs_s,
                            nmse=nmse, iters=max_iter, fused=sol.fuse,
-                           fin=sol.fin and max_iter >= 2)
+                           loop=sol.loop and max_iter >= 2)
     return _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c, lr_s,
                             max_iter, betas, eps, project_c, restart, restart_samples, T_true,
                             nmse_every, callback)

@@ -71,8 +71,8 @@ int main(void) {
     assert vals[3] == _lib.STATE_BYTES
     assert vals[4] == _lib.QscModel.bounds.offset
     assert vals[5] == _lib.QscObsDesc.nnz.offset
-    # the words the fused-finish launch addresses by index (csrc/qsc_pass.hip scfin_kernel:
-    # int word 9, 64-bit word 5) and _lib.read_state decodes
+    # the words _lib.read_state decodes by index (the persistent loop's fault word: int word 9;
+    # the reserved 64-bit word 5)
     assert vals[6] == 36 and vals[7] == 40
 
 

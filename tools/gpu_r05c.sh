@@ -8,6 +8,10 @@ mkdir -p $G
 export TMPDIR=/tmp
 stop() { echo "STOP rc=$1 at $2"; exit $1; }
 cd $R
+if [ -x tools/micro/grid_sync ]; then
+  timeout -k 5 60 ./tools/micro/grid_sync > $G/grid_sync.log 2>&1 || { cat $G/grid_sync.log; stop 1 grid_sync; }
+  cat $G/grid_sync.log
+fi
 echo "# HEAD $(cat .head_sha 2>/dev/null)" > $G/head.txt
 timeout -k 10 400 python bench.py --config c5 --steps 200 --warmup 20 > $G/bench_c5.log 2>&1 || { tail -20 $G/bench_c5.log; stop 1 bench_c5; }
 tail -1 $G/bench_c5.log | cut -c1-300

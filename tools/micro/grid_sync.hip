@@ -137,6 +137,69 @@ __global__ void __launch_bounds__(kThreads) k_greduce(unsigned long long* ctr, f
   }
 }
 
+// one launch per iteration: head = every workgroup sums the 16 group partials of the previous
+// launch (plain loads: the kernel boundary publishes them), body = write this tile's partial
+// write-through, tail = the last arrival of each group sums its group's 16 partials (sc1 buffer
+// loads, all in flight) into this launch's group record (ping-pong: gin / gout)
+__device__ __forceinline__ float ld_sc1(const float* base, unsigned off_bytes) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0,
+                                                                     0x7fffffff, 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off_bytes, 0, 16);  // aux 16: sc1
+}
+__global__ void __launch_bounds__(kThreads) k_one(unsigned long long* ctr, float* part,
+                                                   const float* gin, float* gout, float* cout) {
+  const int t = blockIdx.x, nt = gridDim.x, tid = threadIdx.x;
+  __shared__ int last;
+  float s0 = 0.0f, s1 = 0.0f;
+  {
+    float v0[kGroups], v1[kGroups];
+#pragma unroll
+    for (int g = 0; g < kGroups; ++g) {
+      v0[g] = gin[(size_t)g * kCols + tid];
+      v1[g] = gin[(size_t)g * kCols + tid + kThreads];
+    }
+#pragma unroll
+    for (int g = 0; g < kGroups; ++g) {
+      s0 += v0[g];
+      s1 += v1[g];
+    }
+  }
+  if (t == 0) {
+    cout[tid] = s0 * 1e-6f;
+    cout[tid + kThreads] = s1 * 1e-6f;
+  }
+  st_wt(part + (size_t)t * kCols + tid, s0 * 0.5f + t);
+  st_wt(part + (size_t)t * kCols + tid + kThreads, s1 * 0.5f + t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int g = t % kGroups;
+  const int ng = (nt - g + kGroups - 1) / kGroups;
+  if (tid == 0) {
+    const unsigned long long v = __hip_atomic_fetch_add(ctr + 16 * g, 1ull, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+    last = ((v + 1) % (unsigned long long)ng) == 0;
+  }
+  __syncthreads();
+  if (last) {
+    float a0[kGroups], a1[kGroups];
+#pragma unroll
+    for (int j = 0; j < kGroups; ++j) {
+      const int tt = min(g + j * kGroups, nt - 1);
+      a0[j] = ld_sc1(part, (unsigned)(((size_t)tt * kCols + tid) * 4));
+      a1[j] = ld_sc1(part, (unsigned)(((size_t)tt * kCols + tid + kThreads) * 4));
+    }
+    float x0 = 0.0f, x1 = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kGroups; ++j)
+      if (g + j * kGroups < nt) {
+        x0 += a0[j];
+        x1 += a1[j];
+      }
+    gout[(size_t)g * kCols + tid] = x0;
+    gout[(size_t)g * kCols + tid + kThreads] = x1;
+  }
+}
+
 // pair form: tile kernel + finish kernel
 __global__ void __launch_bounds__(kThreads) k_tile(const float* cin, float* part) {
   const int t = blockIdx.x, tid = threadIdx.x;
@@ -205,6 +268,33 @@ int main() {
   CHECK(hipEventSynchronize(e1));
   CHECK(hipEventElapsedTime(&ms, e0, e1));
   printf("pair (tile + finish launches, hipGraph): %7.2f us / iteration\n", ms * 1e3f / iters);
+
+  // one launch per iteration (head combine + group tail), ping-pong group records, in a graph
+  {
+    float* g2;
+    CHECK(hipMalloc(&g2, (size_t)2 * kGroups * kCols * 4));
+    CHECK(hipMemset(g2, 0, (size_t)2 * kGroups * kCols * 4));
+    CHECK(hipMemset(ctr, 0, 1 << 16));
+    hipGraph_t g1;
+    hipGraphExec_t x1;
+    CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+    for (int i = 0; i < iters; ++i) {
+      float* gi = g2 + (size_t)(i & 1) * kGroups * kCols;
+      float* go = g2 + (size_t)((i + 1) & 1) * kGroups * kCols;
+      hipLaunchKernelGGL(k_one, dim3(nt), dim3(kThreads), 0, s, ctr, part, gi, go, cbuf);
+    }
+    CHECK(hipStreamEndCapture(s, &g1));
+    CHECK(hipGraphInstantiate(&x1, g1, nullptr, nullptr, 0));
+    CHECK(hipGraphLaunch(x1, s));
+    CHECK(hipStreamSynchronize(s));
+    CHECK(hipEventRecord(e0, s));
+    CHECK(hipGraphLaunch(x1, s));
+    CHECK(hipEventRecord(e1, s));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    printf("one launch (head combine + group tail, hipGraph): %7.2f us / iteration\n",
+           ms * 1e3f / iters);
+  }
 
   for (int rep = 0; rep < 2; ++rep) {
     CHECK(hipMemsetAsync(ctr, 0, 1 << 16, s));

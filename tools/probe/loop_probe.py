@@ -36,28 +36,18 @@ def main():
     p = synthetic.onebit_problem(I, J, K, R, f=0.1, seed=5, keep_T=False)
     tile = int(os.environ.get("LOOP_TILE", "0")) or None
     o = Observations(p["Y"], p["Wx"], p["b"], p["sigma"], R_hint=R, tile=tile)
-    a = FreeSSolver(o, p["S0"], p["C0"], hist_cap=4096, fin=False, loop=False)
+    a = FreeSSolver(o, p["S0"], p["C0"], hist_cap=4096, loop=False)
     b = FreeSSolver(o, p["S0"], p["C0"], hist_cap=4096, loop=True)
     print("tiles", o.desc.ntiles, "loop applies", b.loop, flush=True)
     if not b.loop:
         return 1
     a.run(n)
-    prog = torch.zeros(o.desc.ntiles, dtype=torch.int32, device="cuda")
-    b.c_step()
-    b.engine.scpass_loop(b.S, b.C, b.mS, b.vS, b.adam_s, b.lambda_s, b.mC, b.vC, b.adam_c,
-                         b.lambda_c, n - 1, progress=prog)
-    b.s_step()
+    b.run(n)
     torch.cuda.synchronize()
-    pv = prog.cpu().tolist()
-    import collections
-    print("progress (16 * iteration + phase: count)", sorted(collections.Counter(pv).items()),
-          flush=True)
-    print("laggards", [(i, v) for i, v in enumerate(pv) if v != max(pv)][:20], flush=True)
     sb = b.state()
-    tk, dn = b.engine.fin_counters()
-    nvb = R * o.desc.nks + 2
-    print("fused_fault", sb["fused_fault"], "tickets", tk, "expected", (n - 1) * o.desc.ntiles,
-          "finish items done", dn, "expected", (n - 1) * nvb, flush=True)
+    arr, grp = b.engine.loop_counters()
+    print("fused_fault", sb["fused_fault"], "arrivals", arr, "expected", (n - 1) * o.desc.ntiles,
+          "groups", grp, "expected", (n - 1) * min(o.desc.ntiles, 16), flush=True)
     same = all(torch.equal(x, y) for x, y in ((a.S, b.S), (a.C, b.C), (a.mS, b.mS), (a.vS, b.vS),
                                               (a.mC, b.mC), (a.vC, b.vC)))
     print("bitexact", same, "state equal", a.state() == sb,
