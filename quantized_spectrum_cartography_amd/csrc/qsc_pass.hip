@@ -2347,7 +2347,8 @@ __device__ __forceinline__ float ld_sc1b(const float* base, int64_t idx) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base),
                                                                      (short)0, 0x7fffffff,
                                                                      0x00020000);
-  return __builtin_amdgcn_raw_buffer_load_b32(r, (int)(idx * 4), 0, 16);  // aux 16: sc1
+  // (the builtin returns the 32 bits as an unsigned int: reinterpret, do not convert)
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(idx * 4), 0, 16));  // aux 16: sc1
 }
 
 // ||C||^2 of the LDS C^T as scfused_tile's t == 0 forms it (threads < 256 over flat indices

@@ -144,7 +144,7 @@ __global__ void __launch_bounds__(kThreads) k_greduce(unsigned long long* ctr, f
 __device__ __forceinline__ float ld_sc1(const float* base, unsigned off_bytes) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0,
                                                                      0x7fffffff, 0x00020000);
-  return __builtin_amdgcn_raw_buffer_load_b32(r, off_bytes, 0, 16);  // aux 16: sc1
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off_bytes, 0, 16));  // sc1
 }
 __global__ void __launch_bounds__(kThreads) k_one(unsigned long long* ctr, float* part,
                                                    const float* gin, float* gout, float* cout) {
