@@ -104,10 +104,9 @@ typedef struct qsc_state {
   float nll_c;      /* NLL of the last C-pass   (-sum Wx log P, qmc/qmc.ipynb :572) */
   float nll_s;      /* NLL of the last S-pass */
   float normsq_s_prev; /* ||S||^2 the last S-pass was evaluated with */
-  int32_t fused_fault; /* sticky: 1 after a qsc_scpass_loop launch whose wait timed out (its
-                          C updates are then incomplete: results invalid) */
-  uint64_t fin_ticket; /* retired (round 3's fused-finish ticket; the arrival counters now live
-                          on lines of their own in the pass workspace, qsc_pass_sync_offset) */
+  int32_t fused_fault; /* reserved, 0 (the fault word of round 4-5's one-launch forms, which
+                          were measured slower than the launch pairs and removed) */
+  uint64_t fin_ticket; /* reserved, 0 */
   float reserved[4];
 } qsc_state;
 
@@ -356,31 +355,6 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
                        int32_t split_rows, const qsc_model* m, int32_t R, float* S,
                        const float* C, float* mS, float* vS, const qsc_adam* adam,
                        float lambda_s, qsc_state* st, void* ws, size_t ws_bytes, void* stream);
-/* n_iter fused bodies in ONE persistent launch: per body the S-step and the next C-pass
- * (qsc_scpass) and that C-pass's C-step finish (qsc_cfinish mode 1) -- the same operands,
- * arithmetic and summation order, so the same S, C, moments, state and history bit for bit as
- * n_iter x (qsc_scpass, qsc_cfinish).  One workgroup per tile for the whole launch; no
- * workgroup runs the finish alone: each tile group's last arrival sums its group's dC
- * partials and scalar tile sums (write-through, its arrival ticket tells it, nobody waits), and
- * at the next body every workgroup sums the 16 group records and runs the C update itself
- * (bit-identical on every workgroup) after ONE poll of the completed-group counter.  All tiles
- * must be resident at once: qsc_scpass_loop_supported(d, R) requires the fused launch at rank
- * <= 8 with its loop state fitting the LDS and ntiles <= the device's CU count, and the launch
- * checks the kernel instance's occupancy (QSC_EUNSUPPORTED otherwise).  A wait past ~2 * 10^6
- * polls sets st->fused_fault and ends the launch (results invalid).  At exit C, mC, vC and *st
- * are those n_iter x (qsc_scpass, qsc_cfinish) leave before the LAST qsc_cfinish, which the
- * caller issues next (its slab is the last body's): a solver runs  cpass, cfinish,
- * scpass_loop(n-1), cfinish, spass  for n iterations.  hist / hist_cap as qsc_cfinish.
- * Replaces the notebook's S-step and next C-step, n-1 times (qmc/qmc.ipynb :562-634). */
-QSC_API int qsc_scpass_loop_supported(const qsc_obs_desc* d, int32_t R);
-QSC_API int qsc_scpass_loop(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
-                            const int64_t* s_off, const void* c_entries, const int32_t* c_width,
-                            const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
-                            int32_t R, float* S, float* C, float* mS, float* vS,
-                            const qsc_adam* adam_s, float lambda_s, float* mC, float* vC,
-                            const qsc_adam* adam_c, float lambda_c, qsc_state* st, float* hist,
-                            int32_t hist_cap, int32_t n_iter, void* ws, size_t ws_bytes,
-                            void* stream);
 /* reduce the C-pass slab (fixed order).  mode 0: write dC (NLL gradient only); mode 1: fused
  * C-step: dC + lambda_c*C/||C||, Adam on C, projection; mode 2 (IJ-slab sharding): as mode 0 and
  * dC[R*K] (dC holds R*K + 1 floats) receives this shard's ||S||^2 after the S-pass partials are
@@ -430,11 +404,6 @@ QSC_API int qsc_cpass_nsq(const qsc_obs_desc* d, const void* c_entries, const in
                           const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
                           int32_t R, const float* S, const float* C, void* ws, size_t ws_bytes,
                           void* stream);
-/* byte offset in the pass workspace of the persistent loop's counters, for diagnostics: uint64
- * words each on a 128-B line of its own -- word 16 g (g < 16): the arrivals of tile group g
- * (tiles t with t mod 16 == g), word 256: completed groups; counted from zero per launch.  -1 on
- * an invalid descriptor. */
-QSC_API int64_t qsc_pass_sync_offset(const qsc_obs_desc* d, int32_t R);
 /* byte offset, in the pass workspace, of the float where qsc_cpass / qsc_cpass_nsq leave ||C||^2
  * of the C they read (the fixed order of qsc_sumsq_small): a K-slab solver all-reduces it in
  * place and hands it to qsc_cfinish as normsq_c_ext.  -1 on an invalid descriptor. */

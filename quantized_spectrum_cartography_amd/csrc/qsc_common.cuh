@@ -502,31 +502,6 @@ __device__ __forceinline__ T block_sum(T v, T* sh) {
   return r;  // valid in thread 0
 }
 
-// The same sums for a caller-supplied thread index `tid` (== threadIdx.x): the lane indices of
-// the shuffles derive from it, so that a persistent kernel which re-derives `tid` each iteration
-// keeps them from being hoisted out of its loop (and spilled); ds_bpermute is what __shfl_xor
-// issues at width 64, hence the same values bit for bit
-__device__ __forceinline__ float wave_sum_tid(float v, unsigned tid) {
-  const int lane = (int)(tid & 63);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-    v += __int_as_float(__builtin_amdgcn_ds_bpermute((lane ^ o) << 2, __float_as_int(v)));
-  return v;
-}
-__device__ __forceinline__ float block_sum_tid(float v, float* sh, unsigned tid) {
-  v = wave_sum_tid(v, tid);
-  const int w = (int)(tid >> 6), l = (int)(tid & 63);
-  __syncthreads();
-  if (l == 0) sh[w] = v;
-  __syncthreads();
-  float r = 0;
-  if (tid == 0) {
-    const int nw = (blockDim.x + 63) >> 6;
-    for (int i = 0; i < nw; ++i) r += sh[i];
-  }
-  return r;  // valid in thread 0
-}
-
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 __host__ __device__ inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
 
@@ -630,24 +605,8 @@ __device__ __forceinline__ AdamScalars adam_scalars_cached(const AdamCache& c, c
   return adam_scalars(ad, step);
 }
 
-// DEV: field by field as agent-scope write-through stores (read by other workgroups of a
-// persistent launch, qsc_scpass_loop)
-template <bool DEV = false>
 __device__ __forceinline__ void adam_cache_store(AdamCache* slots, const qsc_adam& ad, int step) {
-  const AdamCache c = adam_cache_make(ad, step, adam_scalars(ad, step));
-  if constexpr (DEV) {
-    AdamCache* d = slots + (step & 1);
-    __hip_atomic_store(&d->tag, c.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&d->lr, c.lr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&d->b1, c.b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&d->b2, c.b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&d->eps, c.eps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&d->step_size, c.step_size, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&d->bc2_sqrt, c.bc2_sqrt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&d->rbc2, c.rbc2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    slots[step & 1] = c;
-  }
+  slots[step & 1] = adam_cache_make(ad, step, adam_scalars(ad, step));
 }
 
 // One Adam element update (torch 2.x single-tensor path):

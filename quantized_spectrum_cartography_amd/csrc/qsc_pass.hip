@@ -1465,31 +1465,6 @@ size_t cpass_tile_lds(int PT, int R, int nks, int NP, bool sr) {
 // ---------------------------------------------------------------------------------------
 // fused launch block: 16 waves (4 per SIMD, 128 VGPRs) up to rank 8; 8 waves at rank 16, whose
 // two slice register sets and 16-float rows need up to 256 VGPRs (2 waves per SIMD)
-// Stores of the values other workgroups of the persistent loop read within the launch
-// (qsc_scpass_loop: dC slab rows, NLL / norm partials): with FIN they are agent-scope relaxed
-// atomic stores, i.e. written through this XCD's L2 to the device coherence point, so that
-// workgroups on other XCDs see them once the stores have completed (s_waitcnt) -- no L2
-// write-back fence per workgroup (measured in round 4: with one `buffer_wbl2` per workgroup a
-// one-launch iteration took 40 us against 31 + 3 for the launch pair).  Without FIN: plain
-// stores.  ... and their loads in the reading workgroups: agent-scope relaxed atomic loads (sc1, served
-// by the XCD's L2, never by the CU's L1), so that with write-through stores on the producer side
-// and the vmcnt-drained ticket no acquire fence is needed (MI355X_MICROARCH.md, hand-off forms:
-// every load of the handed-off bytes sc1, every store sc1, one lane signalling behind a barrier)
-template <bool FIN, typename T>
-__device__ __forceinline__ T ld_fin(const T* p) {
-  if constexpr (FIN)
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    return *p;
-}
-
-template <bool FIN, typename T>
-__device__ __forceinline__ void st_fin(T* p, T v) {
-  if constexpr (FIN)
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    *p = v;
-}
 
 template <int RP>
 struct FusedBlock {
@@ -1522,33 +1497,12 @@ struct FusedBlock {
   s_ent, s_width, s_off, c_ent, c_width, c_off, c_kmap, nks, NP, PT, lk, E_, nbins, R, K, S, C, mS, \
       vS, ad, lambda_s, st, part_nll_s, part_nsq_s, slab, part_nll_c, cnsq, acache, c_split
 
-// The persistent loop's per-workgroup state in LDS (scloop_kernel, after the tile's LDS): the
-// solver state as the launch pairs would leave it in qsc_state (every workgroup keeps its own,
-// identical copy; workgroup 0 writes it back at the end), the next iteration's Adam scalars,
-// the C-step scalars of the head, and the tile's per-slice / per-k-slice NLL and ||S||^2
-// partials for its canonical tile sums (canon_totals).
-struct LoopState {
-  int step_s, step_c, iter, pending;
-  float normsq_s, normsq_c, nll_c, nll_s, normsq_s_prev;
-  int fault, last, pad_;
-  AdamScalars as_s, as_c;  // the next iteration's S-step / C-step Adam scalars
-  Scalars scc;             // the head's C-step regulariser coefficient and Adam scalars
-  float sh[16];            // block_sum scratch of the head
-  float ts[1];             // [2 nsl] per-slice NLL, ||S||^2; then [nks] per-k-slice C-pass NLL
-};
-size_t loop_lds(int nsl, int nks) {
-  return (sizeof(LoopState) + (size_t)(2 * nsl + nks) * 4 + 15) & ~(size_t)15;
-}
 
-// One pixel tile t of nt of the fused launch (scfused_kernel; scloop_kernel: t = the workgroup).
-// C is read-only here.  LOOP (scloop_kernel): every cross-workgroup value is stored write-through
-// (FIN), qsc_state is not touched (the state lives in `ll`), the tile's scalar partials also go to
-// `ll`; with `head` the caller has already staged the new C^T and the S-step scalars (iterations
-// after the first: the LDS tables' static parts stay from the first).
-template <int RP, typename E, int KIND, bool LOG, bool FIN = false, bool LOOP = false>
+// One pixel tile t of nt of the fused launch (scfused_kernel: t = the workgroup).  C is
+// read-only here.
+template <int RP, typename E, int KIND, bool LOG>
 __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const int nt,
-                                             const unsigned tidx, const bool head = false,
-                                             LoopState* ll = nullptr) {
+                                             const unsigned tidx) {
   using V4 = typename Ent<E>::V4;
   constexpr int CP = TP<RP, KIND>::v;  // C^T row pitch == S tile row pitch
   constexpr int RH = RP / 2;
@@ -1581,8 +1535,6 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   // 1. C^T / edge / state reads first (the LDS staging then waits only for them: vmcnt
   //    retires in issue order), then the first slice's reads, then the staging
   const int k0 = tidx;
-  // LOOP iterations after the first: C^T, the tables' static parts and the scalars are staged
-  const bool stage_c = !(LOOP && head);
 #if QSC_CT_VEC
   // C^T from 16-B reads of the [R][K] C: thread i holds C's flat floats 4i..4i+3 (one row r,
   // four consecutive bins) and writes them transposed; 32x fewer read instructions than a
@@ -1591,10 +1543,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   const bool cvec = (K & 3) == 0 && ((reinterpret_cast<uintptr_t>(C) & 15) == 0);
   float4 cq = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   float c0[RP];
-  if (!stage_c) {
-#pragma unroll
-    for (int r = 0; r < RP; ++r) c0[r] = 0.0f;
-  } else if (cvec) {
+  if (cvec) {
     cq = reinterpret_cast<const float4*>(C)[min(k0, n4 - 1)];
   } else {
 #pragma unroll
@@ -1621,7 +1570,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   float nsq_s = 0.0f;
   int step_s = 0;
   AdamCache ac0{}, ac1{};
-  if (tidx == 0 && stage_c) {
+  if (tidx == 0) {
     nsq_s = st->normsq_s;
     step_s = st->step_s;
     ac0 = acache[0];  // both slots: no dependent read on step_s
@@ -1637,7 +1586,6 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   // burst is then a quarter of the tile's slice data and the S-step starts that much earlier.
   const bool early = w < QSC_EARLY_WAVES;
   auto stage = [&]() {
-    if (!stage_c) return;  // (LOOP, after the first iteration: staged by the head)
 #if QSC_CT_VEC
     if (cvec) {
       const int Ko = sr_off(K);  // the negated half of a signed-row C^T table
@@ -1697,28 +1645,14 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
       const float nrm = sqrtf(nsq_s);
       sc.coef = nrm > 0.0f ? lambda_s / nrm : 0.0f;
       sc.as = adam_scalars_cached(((step_s + 1) & 1) ? ac1 : ac0, ad, step_s + 1);
-      if constexpr (LOOP) {
-        // the state after this S-step's start (what t == 0 stores in the launch form below),
-        // kept by every workgroup; workgroup 0 writes it back at the end of the loop
-        const int pend = st->pending;
-        ll->step_s = step_s;
-        ll->step_c = st->step_c + ((pend & QSC_PEND_C) ? 1 : 0);
-        ll->pending = (pend & ~QSC_PEND_C) | QSC_PEND_SNLL | QSC_PEND_SUPD;
-        ll->normsq_s = nsq_s;
-        ll->normsq_s_prev = nsq_s;
-        ll->iter = st->iter + 1;
-        ll->nll_c = st->nll_c;
-        ll->nll_s = st->nll_s;
-        ll->normsq_c = st->normsq_c;
-        ll->fault = 0;
-      } else if (t == 0) {
+      if (t == 0) {
         // book-keeping of spass_kernel (mode 1)
         int pend = st->pending;
-        if (pend & QSC_PEND_C) st_fin<FIN>(&st->step_c, st->step_c + 1);
+        if (pend & QSC_PEND_C) st->step_c += 1;
         pend &= ~QSC_PEND_C;
-        st_fin<FIN>(&st->pending, pend | QSC_PEND_SNLL | QSC_PEND_SUPD);
-        st_fin<FIN>(&st->normsq_s_prev, nsq_s);
-        st_fin<FIN>(&st->iter, st->iter + 1);
+        st->pending = pend | QSC_PEND_SNLL | QSC_PEND_SUPD;
+        st->normsq_s_prev = nsq_s;
+        st->iter = st->iter + 1;
       }
     }
     STAMP(wg, 11);  // (wave 0: the scalars are set)
@@ -1743,9 +1677,8 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
         const float c = Cl[k * CP + r];
         s2 = __builtin_fmaf(c, c, s2);
       }
-    // (the same sum either way; the loop's form keeps its lane indices in the iteration)
-    const float nsq = LOOP ? block_sum_tid(s2, Nl, tidx) : block_sum(s2, Nl);
-    if (tidx == 0) st_fin<FIN>(cnsq, nsq);
+    const float nsq = block_sum(s2, Nl);
+    if (tidx == 0) *cnsq = nsq;
   }
 
   // 2. S-step over the wave's slices (next slice's reads in flight; the two register sets
@@ -1805,15 +1738,9 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
       st_row<RH>(Sl + (sr_off(PT) + il * QSC_SLICE + p) * CP + h * RH, nv);
     }
     nsq = wave_sum_dpp(nsq);
-    if (lane == 0) st_fin<FIN>(&part_nsq_s[s], nsq);
+    if (lane == 0) part_nsq_s[s] = nsq;
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
-    if (lane == 0) st_fin<FIN>(&part_nll_s[s], nll_w);
-    if constexpr (LOOP) {
-      if (lane == 0) {
-        ll->ts[il] = nll_w;
-        ll->ts[nsl + il] = nsq;
-      }
-    }
+    if (lane == 0) part_nll_s[s] = nll_w;
     STAMP(wg, 5 + min(n, 8));  // end of the wave's n-th slice
     il = il1;
     ++n;
@@ -1909,7 +1836,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
 
   // the next launch's S-step scalars, by the oldest wave of block 0 (it has slack: its slices
   // are done long before the tile barrier)
-  if (!LOOP && t == 0 && tidx == 0) adam_cache_store<FIN>(acache, ad, step_s + 2);
+  if (t == 0 && tidx == 0) adam_cache_store(acache, ad, step_s + 2);
 
   STAMP(wg, 2);
   if (u < U) {
@@ -1926,13 +1853,10 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     if (NP == 1) {
 #pragma unroll
       for (int j = 0; j < RP / 2; ++j) {
-        if (2 * j < R) st_fin<FIN>(&slab[((int64_t)t * R + 2 * j) * Kp + k], accp[j].x);
-        if (2 * j + 1 < R) st_fin<FIN>(&slab[((int64_t)t * R + 2 * j + 1) * Kp + k], accp[j].y);
+        if (2 * j < R) slab[((int64_t)t * R + 2 * j) * Kp + k] = accp[j].x;
+        if (2 * j + 1 < R) slab[((int64_t)t * R + 2 * j + 1) * Kp + k] = accp[j].y;
       }
-      if (lane == 0) st_fin<FIN>(&part_nll_c[wi], nll_w);
-      if constexpr (LOOP) {
-        if (lane == 0) ll->ts[2 * nsl + u] = nll_w;  // (NP == 1: unit u is k-slice u)
-      }
+      if (lane == 0) part_nll_c[wi] = nll_w;
     } else {
       to_pl(accp);
       if (lane == 0) Nl[u] = nll_w;
@@ -1953,13 +1877,12 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
 #else
       const int kk = c_kmap[((int64_t)t * nks + ks) * 64 + l];
 #endif
-      st_fin<FIN>(&slab[((int64_t)t * R + r) * Kp + kk], acc);
+      slab[((int64_t)t * R + r) * Kp + kk] = acc;
     }
     for (int ks = tidx; ks < nks; ks += blockDim.x) {
       float acc = Nl[ks * NP];
       for (int pp = 1; pp < NP; ++pp) acc += Nl[ks * NP + pp];
-      st_fin<FIN>(&part_nll_c[t * nks + ks], acc);
-      if constexpr (LOOP) ll->ts[2 * nsl + ks] = acc;
+      part_nll_c[t * nks + ks] = acc;
     }
   }
   STAMP(wg, kStampLast);
@@ -1997,93 +1920,67 @@ static bool tile_parts(const qsc_obs_desc* d, int R, bool sr, int* np) {
 }
 
 // ---------------------------------------------------------------------------------------
-// The canonical order of the scalar partials -- the S-passes' per-slice NLL and ||S||^2
-// (part_nll_s, part_nsq_s) and the C-passes' per-(tile, k-slice) NLL (part_nll_c).  Every form
-// settles them in this ONE order, so that the launch pairs (cfinish, state_flush) and the
-// persistent loop (whose tiles, tile groups and workgroups form these sums where the partials
-// are produced: scloop_kernel) agree bit for bit:
-//   tile t:   its items in order (slices slice_of(l, t), l = 0 .. nsl-1; k-slices 0 .. nks-1)
-//   group g:  the tile sums of tiles g, g + kTGroups, g + 2 kTGroups, ... in order
-//   total:    the kTGroups group sums in g order
-// every sum starting from +0.  The groups are the C-finish's tile classes (cfinish sums a dC
-// column over tiles vw, vw + 16, ... per virtual wave vw, then the 16 in order).
+// The fixed order of the scalar partials -- the S-passes' per-slice NLL and ||S||^2
+// (part_nll_s, part_nsq_s) and the C-passes' per-(tile, k-slice) NLL (part_nll_c) -- which every
+// form settles (cfinish's book-keeping block, state_flush: both 1024-thread blocks), so that the
+// solver forms agree bit for bit: thread i sums items i, i + 1024, i + 2048, ... in order (every
+// load of a batch of 8 issued before the sums: one memory round trip at C3's 8192 slices instead
+// of a dependent chain per tile); then each wave's xor butterfly (wave_sum) and the 16 wave sums
+// in wave order; every sum from +0.
 // ---------------------------------------------------------------------------------------
-constexpr int kTGroups = 16;
-__host__ __device__ __forceinline__ int slice_of(int l, int t, int nt) {
-  return l * nt + ((l & 1) ? (nt - 1 - t) : t);
-}
 struct Canon {
   float nll_s, nsq_s, nll_c;
 };
 
-// The three canonical totals, by one workgroup of any size >= kTGroups; ts: LDS [3][blockDim],
-// gs: LDS [3][kTGroups].  Result valid in thread 0.
-__device__ Canon canon_totals(const float* __restrict__ nll_s, const float* __restrict__ nsq_s,
-                              const float* __restrict__ nll_c, int ntiles, int nsl, int nks,
-                              float* ts, float* gs) {
-  const int nb = blockDim.x, tid = threadIdx.x;
-  float ga = 0.0f, gb = 0.0f, gc = 0.0f;  // thread g < kTGroups: running group sums
-  for (int t0 = 0; t0 < ntiles; t0 += nb) {
-    const int t = t0 + tid;
-    if (t < ntiles) {
-      // the tile's items, every load issued before the in-order sums
-      float a = 0.0f, b = 0.0f, c = 0.0f;
-      for (int l0 = 0; l0 < nsl; l0 += 8) {
-        float va[8], vb[8];
+__device__ __forceinline__ float canon_part(const float* __restrict__ x, int n, int tid, int nb) {
+  float a = 0.0f;
+  if (!x) return a;
+  for (int i0 = tid; i0 < n; i0 += 8 * nb) {
+    float v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int s = slice_of(min(l0 + j, nsl - 1), t, ntiles);
-          va[j] = nll_s ? nll_s[s] : 0.0f;
-          vb[j] = nsq_s ? nsq_s[s] : 0.0f;
-        }
+    for (int j = 0; j < 8; ++j) v[j] = x[min(i0 + j * nb, n - 1)];
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (l0 + j < nsl) {
-            a += va[j];
-            b += vb[j];
-          }
-      }
-      if (nll_c)
-        for (int ks = 0; ks < nks; ++ks) c += nll_c[(int64_t)t * nks + ks];
-      ts[tid] = a;
-      ts[nb + tid] = b;
-      ts[2 * nb + tid] = c;
-    }
-    __syncthreads();
-    if (tid < kTGroups) {
-      const int end = min(t0 + nb, ntiles);
-      for (int t1 = t0 + ((tid - t0 % kTGroups) + kTGroups) % kTGroups; t1 < end; t1 += kTGroups) {
-        ga += ts[t1 - t0];
-        gb += ts[nb + t1 - t0];
-        gc += ts[2 * nb + t1 - t0];
-      }
-    }
-    __syncthreads();
+    for (int j = 0; j < 8; ++j)
+      if (i0 + j * nb < n) a += v[j];
   }
-  if (tid < kTGroups) {
-    gs[tid] = ga;
-    gs[kTGroups + tid] = gb;
-    gs[2 * kTGroups + tid] = gc;
+  return a;
+}
+
+// The three totals over nslices S-pass items and nc C-pass items; sh: LDS [3][nb / 64] floats.
+// Result valid in thread 0.
+__device__ Canon canon_totals(const float* __restrict__ nll_s, const float* __restrict__ nsq_s,
+                              const float* __restrict__ nll_c, int nslices, int nc, float* sh) {
+  const int nb = blockDim.x, tid = threadIdx.x, nw = nb >> 6;
+  float a = canon_part(nll_s, nslices, tid, nb);
+  float b = canon_part(nsq_s, nslices, tid, nb);
+  float c = canon_part(nll_c, nc, tid, nb);
+  a = wave_sum(a);
+  b = wave_sum(b);
+  c = wave_sum(c);
+  if ((tid & 63) == 0) {
+    sh[tid >> 6] = a;
+    sh[nw + (tid >> 6)] = b;
+    sh[2 * nw + (tid >> 6)] = c;
   }
   __syncthreads();
   Canon r{0.0f, 0.0f, 0.0f};
   if (tid == 0)
-    for (int g = 0; g < kTGroups; ++g) {
-      r.nll_s += gs[g];
-      r.nsq_s += gs[kTGroups + g];
-      r.nll_c += gs[2 * kTGroups + g];
+    for (int w = 0; w < nw; ++w) {
+      r.nll_s += sh[w];
+      r.nsq_s += sh[nw + w];
+      r.nll_c += sh[2 * nw + w];
     }
   return r;
 }
 
 // book-keeping shared by cfinish (block 0) and state_flush: settle a pending S-pass
 __device__ void settle_s(qsc_state* __restrict__ st, const float* __restrict__ part_nll_s,
-                         const float* __restrict__ part_nsq_s, int ntiles, int nsl, float* hist,
-                         int hist_cap, float* ts, float* gs) {
+                         const float* __restrict__ part_nsq_s, int nslices, float* hist,
+                         int hist_cap, float* sh) {
   const int pend = st->pending;  // uniform read (all threads)
   if (!(pend & (QSC_PEND_SNLL | QSC_PEND_SUPD))) return;
   const Canon c = canon_totals(part_nll_s, (pend & QSC_PEND_SUPD) ? part_nsq_s : nullptr, nullptr,
-                               ntiles, nsl, 0, ts, gs);
+                               nslices, 0, sh);
   if (threadIdx.x == 0) {
     const int it = st->iter - 1;
     st->nll_s = c.nll_s;
@@ -2121,7 +2018,7 @@ constexpr int kFWaves = kFBlock / 64;
 // virtual wave's column partial sums its tiles vw, vw + 16, ... in order; sixteen loads in
 // flight per lane (16 / VF tiles of each virtual wave per batch), so a 4..15-wave workgroup
 // holds no more registers for it than the 16-wave one
-template <bool DEV, int VF>
+template <int VF>
 __device__ __forceinline__ void cfin_tile_sum(float (*red)[64], const float* col,
                                               const int64_t tstride, const int ntiles,
                                               const int wave, const int NWp, const int lane) {
@@ -2143,7 +2040,7 @@ __device__ __forceinline__ void cfin_tile_sum(float (*red)[64], const float* col
           for (int j = 0; j < JB; ++j) {
             const int tt = tg + gb * 16 * NW + vw + (jb + j) * NW;
             v[gb][f][j] =
-                vw < NW ? ld_fin<DEV>(&col[(int64_t)min(tt, ntiles - 1) * tstride]) : 0.0f;
+                vw < NW ? col[(int64_t)min(tt, ntiles - 1) * tstride] : 0.0f;
           }
         }
 #pragma unroll
@@ -2166,9 +2063,8 @@ __device__ __forceinline__ void cfin_tile_sum(float (*red)[64], const float* col
 // passed in: per (r, 64-bin slice) column block the 16 waves' partials (wave w: tiles w, w + 16,
 // ... in order -- the canonical tile groups, canon_totals) summed in wave order; item R*nks the
 // book-keeping (canon_totals), item R*nks + 1 the next C-step's Adam scalars.
-constexpr bool DEV = false;
-__device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scalars& sc,
-                                           float* ts, float* gs, QSC_CF_PARAMS) {
+__device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scalars& sc, float* sh,
+                                           QSC_CF_PARAMS) {
   constexpr int NW = kFWaves;
   const int NWp = NW;
   const int Kp = nks * 64;
@@ -2176,11 +2072,11 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
 
   // ||C||^2 of the C this step differentiates: written by the C-pass (C is read-only there),
   // or the caller's global value (K-slab); never re-read here, where blocks overwrite C
-  const float nsq = normsq_ext ? *normsq_ext : ld_fin<DEV>(cnsq);
+  const float nsq = normsq_ext ? *normsq_ext : *cnsq;
 
   if (vb == R * nks + 1) {
     // the next C-step's Adam scalars (the next S-pass settles step_c + 1 in between)
-    if (mode == 1 && threadIdx.x == 0) adam_cache_store<DEV>(acache, ad, ld_fin<DEV>(&st->step_c) + 2);
+    if (mode == 1 && threadIdx.x == 0) adam_cache_store(acache, ad, st->step_c + 2);
     return;
   }
   if (vb == R * nks) {
@@ -2190,7 +2086,7 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
     const bool settle = (pend & (QSC_PEND_SNLL | QSC_PEND_SUPD)) != 0;
     const bool supd = (pend & QSC_PEND_SUPD) != 0;
     const Canon cs = canon_totals(settle ? part_nll_s : nullptr, supd ? part_nsq_s : nullptr,
-                                  part_nll_c, ntiles, nslices / ntiles, nks, ts, gs);
+                                  part_nll_c, nslices, npart_c, sh);
     if (threadIdx.x == 0) {
       int pnd = pend;
       if (settle) {  // settle_s, thread-0 part
@@ -2231,7 +2127,7 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
   }
   if (threadIdx.x == 0 && mode == 1) {
     const AdamCache a0 = acache[0], a1 = acache[1];  // both slots: no dependent read on step_c
-    const int step = ld_fin<DEV>(&st->step_c) + 1;
+    const int step = st->step_c + 1;
     const float nrm = sqrtf(nsq);
     sc.coef = nrm > 0.0f ? lambda_c / nrm : 0.0f;
     sc.as = adam_scalars_cached((step & 1) ? a1 : a0, ad, step);
@@ -2239,7 +2135,7 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
   // tile sum: (virtual) wave w takes tiles w, w+16, ...; sixteen independent loads in flight
   const float* col = slab + (int64_t)r * Kp + k;
   const int64_t tstride = (int64_t)R * Kp;
-  cfin_tile_sum<DEV, 1>(red, col, tstride, ntiles, wave, NWp, lane);
+  cfin_tile_sum<1>(red, col, tstride, ntiles, wave, NWp, lane);
   __syncthreads();
   if (wave == 0 && k < K) {
     float g = red[0][lane];
@@ -2250,9 +2146,9 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
       float p = p0, m = m0, v = v0;
       g = __fadd_rn(g, __fmul_rn(p, sc.coef));
       adam_elem(p, m, v, g, ad, sc.as);
-      st_fin<DEV>(&C[i], p);
-      st_fin<DEV>(&mC[i], m);
-      st_fin<DEV>(&vC[i], v);
+      C[i] = p;
+      mC[i] = m;
+      vC[i] = v;
     } else {
       dC[i] = g;  // modes 0 and 2
     }
@@ -2262,415 +2158,10 @@ __device__ __forceinline__ void cfinish_vb(const int vb, float (*red)[64], Scala
 __global__ void __launch_bounds__(kFBlock) cfinish_kernel(QSC_CF_PARAMS) {
   __shared__ float red[kFWaves][64];
   __shared__ Scalars sc;
-  __shared__ float ts[3 * kFBlock];
-  __shared__ float gs[3 * kTGroups];
-  cfinish_vb((int)blockIdx.x, red, sc, ts, gs, QSC_CF_ARGS);
+  __shared__ float sh[3 * kFWaves];
+  cfinish_vb((int)blockIdx.x, red, sc, sh, QSC_CF_ARGS);
 }
 
-// ---------------------------------------------------------------------------------------
-// Persistent fused loop (qsc_scpass_loop): n fused bodies -- S-step i + C-pass i+1, and the
-// C-step finish of that C-pass -- in ONE launch, one workgroup per C-pass tile for the whole
-// launch (every workgroup resident: the launcher checks occupancy x CUs >= tiles).  No
-// workgroup waits for C-finish work items: the finish is split so that nobody computes it alone:
-//   tail of iteration i (every tile): its dC slab rows and its tile sums of the scalar partials
-//     (canon_totals' tile level), stored write-through; an arrival ticket on the counter of its
-//     tile group g = t % 16; the group's LAST arrival (told by its ticket, no wait) sums the
-//     group's tiles in order -- the dC columns exactly as cfinish's virtual wave g does, the
-//     scalars at canon_totals' group level -- into the group record G[i & 1][g] (write-through)
-//     and counts the group complete on the top counter;
-//   head of iteration i+1 (every workgroup): one poll of the top counter until every group of
-//     iteration i is complete, then EVERY workgroup sums the 16 group records in g order and
-//     runs the C-step's regulariser + Adam (+ projection) itself -- cfinish's arithmetic on
-//     cfinish's operands in cfinish's order, so every workgroup holds the same new C bit for
-//     bit, straight into its LDS C^T -- and the state book-keeping of cfinish + the S-step's
-//     start (LoopState, workgroup 0 appends the history row).  The new moments mC, vC go to a
-//     ping-pong buffer written by workgroup 0 alone (read one iteration later).
-// Every value another workgroup reads is stored sc1 and loaded sc1 after a counter it polled or
-// a ticket it took, behind `s_waitcnt vmcnt(0)` + the workgroup barrier on the producer side
-// (MI355X_MICROARCH.md, hand-off forms: no release / acquire fence, whose L2 write-back would
-// drain the S-step's 25 MB of rows).  A wait past kLoopSpin polls sets the state's fault word
-// and every workgroup leaves.  After the loop workgroup 0 waits for the last groups (every
-// workgroup has then left its last head) and writes C, mC, vC and qsc_state as the launch pairs
-// would have left them before their last qsc_cfinish -- which the caller then issues, on the
-// slab of the last C-pass, followed by the closing qsc_spass (qmc.issue_iterations).
-// ---------------------------------------------------------------------------------------
-constexpr unsigned kLoopSpin = 1u << 21;
-// PassWs::sync words, each counter on a 128-B line of its own (only atomics and sc1 loads touch
-// them), zeroed by the launcher before every loop launch: [16 g] group g's arrivals,
-// [16 kTGroups] completed groups
-constexpr int kSyncTop = 16 * kTGroups;
-constexpr int kSyncWords = 16 * (kTGroups + 1);
-
-struct LoopArgs {
-  const void* s_ent;
-  const int* s_width;
-  const int64_t* s_off;
-  const void* c_ent;
-  const int* c_width;
-  const int64_t* c_off;
-  const int* c_kmap;
-  float* S;
-  float* C;
-  float* mS;
-  float* vS;
-  qsc_state* st;
-  float* part_nll_s;
-  float* part_nsq_s;
-  float* slab;
-  float* part_nll_c;
-  float* cnsq;
-  AdamCache* acache;
-  float* mC;
-  float* vC;
-  float* hist;
-  float* grec;   // [2][kTGroups][R Kp + 4] group records (dC columns, then nll_c, nll_s, nsq_s)
-  float* tsum;   // [ntiles][4] tile sums (nll_c, nll_s, nsq_s)
-  float* mvbuf;  // [2][2][R K] the moments mC, vC of the head, ping-pong
-  unsigned long long* sync;
-  qsc_adam ad;
-  qsc_adam adc;
-  Lik lk;
-  float lambda_s, lambda_c;
-  int nks, NP, PT, nbins, R, K, hist_cap, n;
-  size_t tile_lds;  // bytes of the tile body's LDS (the LoopState follows)
-  Edges E;
-};
-using LoopKA = const char __attribute__((address_space(4)));
-#define QSC_LA(f) (*(const decltype(LoopArgs::f)*)(const char*)(kb + offsetof(LoopArgs, f)))
-
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// sc1 buffer loads of a group of independent words (the relaxed atomic loads above are waited
-// one by one; these are batched like plain loads).  Byte offsets below 2^31.
-__device__ __forceinline__ float ld_sc1b(const float* base, int64_t idx) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base),
-                                                                     (short)0, 0x7fffffff,
-                                                                     0x00020000);
-  // (the builtin returns the 32 bits as an unsigned int: reinterpret, do not convert)
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(idx * 4), 0, 16));  // aux 16: sc1
-}
-
-// ||C||^2 of the LDS C^T as scfused_tile's t == 0 forms it (threads < 256 over flat indices
-// t, t + 256, ..., then block_sum): the value cfinish reads from the C-pass
-__device__ __forceinline__ float ct_norm_sq(const float* Cl, int CP, int R, int K, float* sh,
-                                            unsigned tidx) {
-  float s2 = 0.0f;
-  if (tidx < 256)
-    for (int i = (int)tidx; i < R * K; i += 256) {
-      const int r = i / K, k = i - r * K;
-      const float c = Cl[k * CP + r];
-      s2 = __builtin_fmaf(c, c, s2);
-    }
-  return block_sum_tid(s2, sh, tidx);
-}
-
-// the head of iteration it >= 1 (see above); false: a wait timed out (leave the loop)
-template <int RP, int KIND>
-__device__ bool loop_head(LoopKA* kb, const int t, const unsigned tidx, const int it,
-                          LoopState* ll, const int nG) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  Scalars& sc = *reinterpret_cast<Scalars*>(smem);
-  float* Cl = smem + 8;
-  constexpr int CP = TP<RP, KIND>::v;
-  const int R = QSC_LA(R), K = QSC_LA(K), nks = QSC_LA(nks);
-  const int Kp = nks * 64, RK = R * K, gsz = R * Kp + 4;
-  unsigned long long* sync = QSC_LA(sync);
-  // (diagnostic builds: the last head's timeline, realtime stamps 17..19)
-  [[maybe_unused]] const int wg = t * (int)(blockDim.x >> 6) + (int)(tidx >> 6);
-  [[maybe_unused]] const bool stamp = it == QSC_LA(n) - 1;
-  if (stamp) RSTAMP(wg, 17);
-  if (tidx == 0) {
-    unsigned polls = 0;
-    while (__hip_atomic_load(sync + kSyncTop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-           (unsigned long long)nG * (unsigned long long)it) {
-      if (++polls > kLoopSpin) {
-        ll->fault = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-  if (ll->fault) return false;
-  if (stamp) RSTAMP(wg, 18);
-  const float* G = QSC_LA(grec) + (size_t)((it - 1) & 1) * kTGroups * gsz;
-  // ||C_i||^2 of the C the last C-pass used (the LDS C^T) and the C-step scalars
-  const float nsq_c = ct_norm_sq(Cl, CP, R, K, ll->sh, tidx);
-  if (tidx == 0) {
-    const float nrm = sqrtf(nsq_c);
-    ll->scc.coef = nrm > 0.0f ? QSC_LA(lambda_c) / nrm : 0.0f;
-    ll->scc.as = ll->as_c;
-  }
-  __syncthreads();
-  // the C-step: per (r, k) the 16 group sums in g order (cfinish's red[0..15]), + coef C, Adam
-  const qsc_adam adc = QSC_LA(adc);
-  const float coef = ll->scc.coef;
-  const AdamScalars asc = ll->scc.as;
-  const float* mvin = it == 1 ? nullptr : QSC_LA(mvbuf) + (size_t)((it - 1) & 1) * 2 * RK;
-  float* mvout = QSC_LA(mvbuf) + (size_t)(it & 1) * 2 * RK;
-  const float* mC = QSC_LA(mC);
-  const float* vC = QSC_LA(vC);
-  const int Ko = sr_off(K);
-  constexpr int kCols = 2;  // columns per pass per thread (16 group loads each in flight)
-  for (int b0 = 0; b0 < RK; b0 += kCols * (int)blockDim.x) {  // (uniform trip count: barrier)
-    const int i0 = b0 + (int)tidx;
-    float gv[kCols][kTGroups];
-    float m[kCols], v[kCols], p[kCols];
-#pragma unroll
-    for (int c = 0; c < kCols; ++c) {
-      const int i = min(i0 + c * (int)blockDim.x, RK - 1);
-      const int r = i / K, k = i - r * K;
-      const int col = r * Kp + k;
-#pragma unroll
-      for (int g = 0; g < kTGroups; ++g) gv[c][g] = ld_sc1b(G, (int64_t)g * gsz + col);
-      m[c] = mvin ? ld_sc1b(mvin, i) : mC[i];
-      v[c] = mvin ? ld_sc1b(mvin, RK + i) : vC[i];
-      p[c] = Cl[k * CP + r];
-    }
-#pragma unroll
-    for (int c = 0; c < kCols; ++c) {
-      float g = gv[c][0];
-#pragma unroll
-      for (int gg = 1; gg < kTGroups; ++gg) g += gv[c][gg];
-      g = __fadd_rn(g, __fmul_rn(p[c], coef));
-      adam_elem(p[c], m[c], v[c], g, adc, asc);
-    }
-    __syncthreads();  // every thread has read its old C^T entries of this pass
-#pragma unroll
-    for (int c = 0; c < kCols; ++c) {
-      const int i = i0 + c * (int)blockDim.x;
-      if (i >= RK) continue;
-      const int r = i / K, k = i - r * K;
-      Cl[k * CP + r] = p[c];
-      if constexpr (is_sr(KIND)) Cl[(Ko + k) * CP + r] = -p[c];
-      if (t == 0) {
-        __hip_atomic_store(mvout + i, m[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(mvout + RK + i, v[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  if (tidx == 0) {
-    // cfinish's book-keeping block (the settle of the last S-step, the C-pass NLL), then the
-    // S-step's start (scfused_tile, t == 0), on the group records' scalars summed in g order
-    float sv[3][kTGroups];
-#pragma unroll
-    for (int g = 0; g < kTGroups; ++g)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) sv[j][g] = ld_sc1b(G, (int64_t)g * gsz + R * Kp + j);
-    float nll_c = 0.0f, nll_s = 0.0f, nsq_s = 0.0f;
-#pragma unroll
-    for (int g = 0; g < kTGroups; ++g) {
-      nll_c += sv[0][g];
-      nll_s += sv[1][g];
-      nsq_s += sv[2][g];
-    }
-    int pend = ll->pending;
-    if (pend & (QSC_PEND_SNLL | QSC_PEND_SUPD)) {
-      const int hi = ll->iter - 1;
-      float* hist = QSC_LA(hist);
-      if (t == 0 && hist && hi >= 0 && hi < QSC_LA(hist_cap)) {
-        hist[4 * hi + 0] = ll->nll_c;
-        hist[4 * hi + 1] = nll_s;
-        hist[4 * hi + 2] = ll->normsq_c;
-        hist[4 * hi + 3] = ll->normsq_s_prev;
-      }
-      ll->nll_s = nll_s;
-      if (pend & QSC_PEND_SUPD) {
-        ll->normsq_s = nsq_s;
-        ll->step_s += 1;
-      }
-      pend &= ~(QSC_PEND_SNLL | QSC_PEND_SUPD);
-    }
-    ll->nll_c = nll_c;
-    ll->normsq_c = nsq_c;
-    pend |= QSC_PEND_C;
-    // the S-step's start
-    ll->step_c += 1;  // (the C update of this head)
-    pend = (pend & ~QSC_PEND_C) | QSC_PEND_SNLL | QSC_PEND_SUPD;
-    ll->pending = pend;
-    ll->normsq_s_prev = ll->normsq_s;
-    ll->iter += 1;
-    const float nrm = sqrtf(ll->normsq_s);
-    sc.coef = nrm > 0.0f ? QSC_LA(lambda_s) / nrm : 0.0f;
-    sc.as = ll->as_s;
-  }
-  __syncthreads();
-  if (stamp) RSTAMP(wg, 19);
-  return true;
-}
-
-// the tail of iteration it: tile sums, arrival ticket, the group record by the last arrival;
-// and (off the critical path, wave 1) the next iteration's Adam scalars
-template <int RP>
-__device__ void loop_tail(LoopKA* kb, const int t, const int nt, const unsigned tidx,
-                          const int it, LoopState* ll, const int nG) {
-  const int R = QSC_LA(R), nks = QSC_LA(nks), Kp = nks * 64, gsz = R * Kp + 4;
-  const int nsl = QSC_LA(PT) / QSC_SLICE;
-  unsigned long long* sync = QSC_LA(sync);
-  float* tsum = QSC_LA(tsum);
-  // (diagnostic builds: the second-to-last tail's timeline, realtime stamps 20..23)
-  [[maybe_unused]] const int wg = t * (int)(blockDim.x >> 6) + (int)(tidx >> 6);
-  [[maybe_unused]] const bool stamp = it == QSC_LA(n) - 2;
-  if (stamp) RSTAMP(wg, 20);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab / partial stores
-  __syncthreads();  // (and the LoopState partials of every wave)
-  if (stamp) RSTAMP(wg, 21);
-  const int g = t % kTGroups;
-  if (tidx == 0) {
-    // canon_totals' tile level: the tile's items in order
-    float a = 0.0f, b = 0.0f, c = 0.0f;
-    for (int l = 0; l < nsl; ++l) {
-      a += ll->ts[l];
-      b += ll->ts[nsl + l];
-    }
-    for (int ks = 0; ks < nks; ++ks) c += ll->ts[2 * nsl + ks];
-    __hip_atomic_store(tsum + 4 * t + 0, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(tsum + 4 * t + 1, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(tsum + 4 * t + 2, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned long long ng = (unsigned long long)((nt - g + kTGroups - 1) / kTGroups);
-    const unsigned long long v =
-        __hip_atomic_fetch_add(sync + 16 * g, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ll->last = ((v + 1) % ng) == 0;
-  }
-  if (tidx == 64 && it + 1 < QSC_LA(n)) {
-    // the next head's C-step and next S-step Adam scalars (the double-precision bias
-    // corrections: ~1 us on one lane, here while the group is being reduced)
-    ll->as_c = adam_scalars(QSC_LA(adc), ll->step_c + 1);
-    ll->as_s = adam_scalars(QSC_LA(ad), ll->step_s + 2);
-  }
-  __syncthreads();
-  if (stamp) RSTAMP(wg, 22);
-  if (!ll->last) return;
-  // the group record: cfinish's virtual wave g on every dC column, canon_totals' group level
-  const float* slab = QSC_LA(slab);
-  float* rec = QSC_LA(grec) + (size_t)(it & 1) * kTGroups * gsz + (size_t)g * gsz;
-  const int ncol = R * Kp;
-  for (int col = tidx; col < ncol; col += blockDim.x) {
-    float v[16];
-    float acc = 0.0f;
-    for (int j0 = g; j0 < nt; j0 += 16 * kTGroups) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int tt = min(j0 + j * kTGroups, nt - 1);
-        v[j] = ld_sc1b(slab, (int64_t)tt * ncol + col);
-      }
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (j0 + j * kTGroups < nt) acc += v[j];
-    }
-    __hip_atomic_store(rec + col, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (tidx < 3) {
-    float acc = 0.0f;
-    for (int j0 = g; j0 < nt; j0 += 16 * kTGroups) {
-      float v[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        v[j] = ld_sc1b(tsum, 4 * (int64_t)min(j0 + j * kTGroups, nt - 1) + tidx);
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (j0 + j * kTGroups < nt) acc += v[j];
-    }
-    __hip_atomic_store(rec + ncol + tidx, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (stamp) RSTAMP(wg, 23);
-  if (tidx == 0)
-    __hip_atomic_fetch_add(sync + kSyncTop, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  (void)nG;
-}
-
-template <int RP, typename E, int KIND, bool LOG>
-__global__ void __launch_bounds__(FusedBlock<RP>::v) scloop_kernel(LoopArgs args) {
-  LoopKA* const kp = (LoopKA*)__builtin_amdgcn_kernarg_segment_ptr();
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  int n = 0;
-  {
-    LoopKA* const kb = kp;
-    n = QSC_LA(n);
-  }
-  (void)args;
-  for (int it = 0; it < n; ++it) {
-    int o = 0, t = (int)blockIdx.x;
-    unsigned tidx = threadIdx.x;
-    asm volatile("" : "+s"(o), "+s"(t), "+v"(tidx));  // re-derived every iteration
-    LoopKA* const kb = kp + o;
-    const int nt = (int)gridDim.x, nG = nt < kTGroups ? nt : kTGroups;
-    LoopState* ll = reinterpret_cast<LoopState*>(reinterpret_cast<char*>(smem) + QSC_LA(tile_lds));
-    if (it > 0 && !loop_head<RP, KIND>(kb, t, tidx, it, ll, nG)) break;
-    scfused_tile<RP, E, KIND, LOG, true, true>(
-        reinterpret_cast<const E*>(QSC_LA(s_ent)), QSC_LA(s_width), QSC_LA(s_off),
-        reinterpret_cast<const E*>(QSC_LA(c_ent)), QSC_LA(c_width), QSC_LA(c_off),
-        QSC_LA(c_kmap), QSC_LA(nks), QSC_LA(NP), QSC_LA(PT), QSC_LA(lk),
-        *(const Edges*)(const char*)(kb + offsetof(LoopArgs, E)), QSC_LA(nbins), QSC_LA(R),
-        QSC_LA(K), QSC_LA(S), QSC_LA(C), QSC_LA(mS), QSC_LA(vS), QSC_LA(ad), QSC_LA(lambda_s),
-        QSC_LA(st), QSC_LA(part_nll_s), QSC_LA(part_nsq_s), QSC_LA(slab), QSC_LA(part_nll_c),
-        QSC_LA(cnsq), QSC_LA(acache), nullptr, t, nt, tidx, it > 0, ll);
-    loop_tail<RP>(kb, t, nt, tidx, it, ll, nG);
-  }
-  // workgroup 0: once every group of the last iteration is complete (every workgroup has left
-  // its last head), the state, C and its moments as the launch pairs leave them before their
-  // last qsc_cfinish; the fault word
-  int o = 0, t = (int)blockIdx.x;
-  unsigned tidx = threadIdx.x;
-  asm volatile("" : "+s"(o), "+s"(t), "+v"(tidx));
-  LoopKA* const kb = kp + o;
-  LoopState* ll = reinterpret_cast<LoopState*>(reinterpret_cast<char*>(smem) + QSC_LA(tile_lds));
-  qsc_state* st = QSC_LA(st);
-  if (t != 0) {
-    if (tidx == 0 && ll->fault)
-      __hip_atomic_store(&st->fused_fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  const int nt = (int)gridDim.x, nG = nt < kTGroups ? nt : kTGroups;
-  unsigned long long* sync = QSC_LA(sync);
-  if (tidx == 0 && !ll->fault) {
-    unsigned polls = 0;
-    while (__hip_atomic_load(sync + kSyncTop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-           (unsigned long long)nG * (unsigned long long)n) {
-      if (++polls > kLoopSpin) {
-        ll->fault = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-  if (ll->fault) {
-    if (tidx == 0) __hip_atomic_store(&st->fused_fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  const int R = QSC_LA(R), K = QSC_LA(K), RK = R * K;
-  constexpr int CP = TP<RP, KIND>::v;
-  const float* Cl = smem + 8;
-  float* C = QSC_LA(C);
-  float* mC = QSC_LA(mC);
-  float* vC = QSC_LA(vC);
-  if (n >= 2) {  // (n == 1: C, mC, vC are those the loop started from)
-    const float* mv = QSC_LA(mvbuf) + (size_t)((n - 1) & 1) * 2 * RK;
-    for (int i = tidx; i < RK; i += blockDim.x) {
-      const int r = i / K, k = i - r * K;
-      C[i] = Cl[k * CP + r];
-      mC[i] = ld_sc1(mv + i);
-      vC[i] = ld_sc1(mv + RK + i);
-    }
-  }
-  if (tidx == 0) {
-    st->step_s = ll->step_s;
-    st->step_c = ll->step_c;
-    st->iter = ll->iter;
-    st->pending = ll->pending;
-    st->normsq_s = ll->normsq_s;
-    st->normsq_c = ll->normsq_c;
-    st->nll_c = ll->nll_c;
-    st->nll_s = ll->nll_s;
-    st->normsq_s_prev = ll->normsq_s_prev;
-  }
-}
-#undef QSC_LA
 
 // ---------------------------------------------------------------------------------------
 // C update from an externally reduced gradient g [R][K] (IJ-slab sharding, after the RCCL
@@ -2712,9 +2203,8 @@ __global__ void __launch_bounds__(1024) flush_kernel(qsc_state* __restrict__ st,
                                                      const float* __restrict__ part_nsq_s,
                                                      int ntiles, int nslices,
                                                      float* __restrict__ hist, int hist_cap) {
-  __shared__ float ts[3 * 1024];
-  __shared__ float gs[3 * kTGroups];
-  settle_s(st, part_nll_s, part_nsq_s, ntiles, nslices / ntiles, hist, hist_cap, ts, gs);
+  __shared__ float sh[3 * 16];
+  settle_s(st, part_nll_s, part_nsq_s, nslices, hist, hist_cap, sh);
   if (threadIdx.x == 0 && (st->pending & QSC_PEND_C)) {
     st->step_c += 1;
     st->pending &= ~QSC_PEND_C;
@@ -2861,20 +2351,9 @@ struct PassWs {
   int* sched;       // S-pass queue counters [kSchedQ] + finished-wave counter (zero between launches)
   float* cnsq;      // ||C||^2 of the C the last C-pass read (written by the C-pass)
   AdamCache* acache;  // [0..1] S-side, [2..3] C-side step scalars (adam_scalars_cached)
-  // the persistent loop's cross-workgroup counters (kSyncWords), each on a 128-B line of its own
-  // that only atomics and agent-scope (sc1) loads touch -- an sc1 load is served by the XCD's
-  // L2, so a counter on a line that plain loads also bring into an L2 can be read stale there
-  // (seen in round 4: a wait that never ended); zeroed by the loop's launcher
-  unsigned long long* sync;
-  float* grec;   // [2][kTGroups][R Kp + 4] the loop's group records
-  float* tsum;   // [ntiles][4] the loop's tile sums
-  float* mvbuf;  // [2][2][R K] the loop's C-side moments, ping-pong
 };
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
-inline size_t grec_bytes(const qsc_obs_desc* d, int R) {
-  return (size_t)2 * kTGroups * ((size_t)R * d->nks * 64 + 4) * 4;
-}
 
 PassWs carve(const qsc_obs_desc* d, int R, void* ws) {
   char* w = (char*)ws;
@@ -2896,13 +2375,6 @@ PassWs carve(const qsc_obs_desc* d, int R, void* ws) {
   w += al(4);
   p.acache = (AdamCache*)w;
   w += al(4 * sizeof(AdamCache));
-  p.sync = (unsigned long long*)w;
-  w += al(kSyncWords * sizeof(unsigned long long));
-  p.grec = (float*)w;
-  w += al(grec_bytes(d, R));
-  p.tsum = (float*)w;
-  w += al((size_t)d->ntiles * 4 * 4);
-  p.mvbuf = (float*)w;
   return p;
 }
 
@@ -2910,8 +2382,7 @@ size_t ws_bytes_for(const qsc_obs_desc* d, int R) {
   const int64_t Kp = (int64_t)d->nks * 64;
   return al((size_t)d->ntiles * R * Kp * 4) + al((size_t)d->ntiles * d->nks * 4) +
          2 * al((size_t)(d->Pp / QSC_SLICE) * 4) + al(256 * 8) + al((kSchedQ + 1) * 4) + al(4) +
-         al(4 * sizeof(AdamCache)) + al(kSyncWords * sizeof(unsigned long long)) +
-         al(grec_bytes(d, R)) + al((size_t)d->ntiles * 4 * 4) + al((size_t)4 * R * d->K * 4);
+         al(4 * sizeof(AdamCache));
 }
 
 bool desc_ok(const qsc_obs_desc* d) {
@@ -3105,12 +2576,6 @@ QSC_API int qsc_cpass_nsq(const qsc_obs_desc* d, const void* c_entries, const in
                     true);
 }
 
-QSC_API int64_t qsc_pass_sync_offset(const qsc_obs_desc* d, int32_t R) {
-  if (!desc_ok(d) || R < 1 || R > QSC_MAX_R) return -1;
-  const uintptr_t base = 4096;
-  return (int64_t)(reinterpret_cast<uintptr_t>(carve(d, R, reinterpret_cast<void*>(base)).sync) -
-                   base);
-}
 
 QSC_API int64_t qsc_pass_cnsq_offset(const qsc_obs_desc* d, int32_t R) {
   if (!desc_ok(d) || R < 1 || R > QSC_MAX_R) return -1;
@@ -3294,120 +2759,6 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
   return QSC_OK;
 }
 
-// every workgroup of the persistent loop resident at once: tiles <= blocks per CU x CUs
-static bool loop_fits(const void* kp, unsigned threads, size_t shm, int ntiles) {
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kp, (int)threads, shm) != hipSuccess)
-    return false;
-  return nb >= 1 && ntiles <= nb * cu_count();
-}
-
-// the loop's LDS: the fused launch's, 16-B aligned, then its LoopState
-static size_t loop_shm(const qsc_obs_desc* d, int R, bool sr, size_t* tile) {
-  const int NP = cpass_parts(d, R, sr);
-  *tile = (scfused_lds(d->PT, R, d->K, d->nks, NP, sr) + 15) & ~(size_t)15;
-  return *tile + loop_lds(d->PT / QSC_SLICE, d->nks);
-}
-
-QSC_API int qsc_scpass_loop_supported(const qsc_obs_desc* d, int32_t R) {
-  if (!qsc_scpass_supported(d, R) || rp_of(R) > 8) return 0;
-  size_t tile = 0;
-  if (loop_shm(d, R, d->rowfmt == 1, &tile) > 160 * 1024) return 0;
-  return d->ntiles <= cu_count() ? 1 : 0;  // at most one workgroup per CU
-}
-
-QSC_API int qsc_scpass_loop(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
-                            const int64_t* s_off, const void* c_entries, const int32_t* c_width,
-                            const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
-                            int32_t R, float* S, float* C, float* mS, float* vS,
-                            const qsc_adam* adam_s, float lambda_s, float* mC, float* vC,
-                            const qsc_adam* adam_c, float lambda_c, qsc_state* st, float* hist,
-                            int32_t hist_cap, int32_t n_iter, void* ws, size_t ws_bytes,
-                            void* stream) {
-  if (!qsc_scpass_loop_supported(d, R) || !m || m->nbounds - 1 != d->nbins || !S || !C || !mS ||
-      !vS || !adam_s || !mC || !vC || !adam_c || !st || !s_width || !s_off || !c_width ||
-      !c_off || !c_kmap || (d->s_entries > 0 && !s_entries) ||
-      (d->c_entries > 0 && !c_entries) || !ws || ws_bytes < ws_bytes_for(d, R) ||
-      (hist_cap > 0 && !hist) || n_iter < 0)
-    return QSC_EINVAL;
-  if (n_iter == 0) return QSC_OK;
-  const int kind = lik_kind(m);
-  const bool sr = d->rowfmt == 1;
-  if (!rowfmt_ok(d, R, kind)) return QSC_EINVAL;
-  const int NP = cpass_parts(d, R, sr);
-  size_t tile_lds = 0;
-  const size_t shm = loop_shm(d, R, sr, &tile_lds);
-  PassWs w = carve(d, R, ws);
-  LoopArgs la{};
-  make_edges(m, &la.E);
-  la.lk = make_lik(m);
-  set_dbg(la.lk, d, sr);
-  if (kind == LIK_SQUARED)
-    make_sq_targets(m, &la.E);
-  else if (!m->log_model)
-    scale_edges(&la.E, m->nbounds - 1, la.lk.a);
-  la.s_ent = s_entries;
-  la.s_width = s_width;
-  la.s_off = s_off;
-  la.c_ent = c_entries;
-  la.c_width = c_width;
-  la.c_off = c_off;
-  la.c_kmap = c_kmap;
-  la.S = S;
-  la.C = C;
-  la.mS = mS;
-  la.vS = vS;
-  la.st = st;
-  la.part_nll_s = w.snll;
-  la.part_nsq_s = w.snsq;
-  la.slab = w.slab;
-  la.part_nll_c = w.cnll;
-  la.cnsq = w.cnsq;
-  la.acache = w.acache;
-  la.mC = mC;
-  la.vC = vC;
-  la.hist = hist;
-  la.grec = w.grec;
-  la.tsum = w.tsum;
-  la.mvbuf = w.mvbuf;
-  la.sync = w.sync;
-  la.ad = *adam_s;
-  la.adc = *adam_c;
-  la.lambda_s = lambda_s;
-  la.lambda_c = lambda_c;
-  la.nks = d->nks;
-  la.NP = NP;
-  la.PT = d->PT;
-  la.nbins = d->nbins;
-  la.R = R;
-  la.K = d->K;
-  la.hist_cap = hist_cap;
-  la.n = n_iter;
-  la.tile_lds = tile_lds;
-  const unsigned threads = scpass_threads(d, R);
-  const int RP = rp_of(R);
-  hipStream_t s = STREAM(stream);
-  // counters from zero, group records zero (tile groups beyond the tile count stay empty)
-  if (hipMemsetAsync(w.sync, 0, kSyncWords * sizeof(unsigned long long), s) != hipSuccess ||
-      hipMemsetAsync(w.grec, 0, grec_bytes(d, R), s) != hipSuccess)
-    return QSC_EINVAL;
-#define SCLOOP_LAUNCH(RPV, ET, KD, LG)                                                         \
-  do {                                                                                         \
-    if constexpr (RPV <= 8) {                                                                  \
-      if (!loop_fits(reinterpret_cast<const void*>(scloop_kernel<RPV, ET, KD, LG>), threads,   \
-                     shm, d->ntiles))                                                          \
-        return QSC_EUNSUPPORTED;                                                               \
-      hipLaunchKernelGGL((scloop_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles),          \
-                         dim3(threads), shm, s, la);                                           \
-    } else {                                                                                   \
-      return QSC_EUNSUPPORTED;                                                                 \
-    }                                                                                          \
-  } while (0)
-  QSC_DISPATCH_PASS(SCLOOP_LAUNCH);
-#undef SCLOOP_LAUNCH
-  QSC_CHECK_LAUNCH();
-  return QSC_OK;
-}
 
 QSC_API int qsc_cfinish(const qsc_obs_desc* d, int32_t R, float* C, int32_t mode, float* dC,
                         float* mC, float* vC, const qsc_adam* adam, float lambda_c,

@@ -105,35 +105,6 @@ class PassEngine:
                   _lib.ptr(vS), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),
                   self.ws.numel(), _lib.stream())
 
-    def scpass_loop_supported(self):
-        return bool(_lib.lib().qsc_scpass_loop_supported(self.desc, self.R))
-
-    def scpass_loop(self, S_pos, C, mS, vS, adam_s, lambda_s, mC, vC, adam_c, lambda_c, n,
-                    record=True):
-        """n fused bodies -- (scpass, cfinish) n times, bit for bit, but for the last cfinish,
-        which the caller issues next -- in ONE persistent launch (qsc_scpass_loop): one
-        workgroup per tile for the whole launch, the C-step finish split over the tile groups'
-        last arrivals and every workgroup's head (include/qsc.h)."""
-        o = self.obs
-        hist, cap = (self.hist, self.hist_cap) if (record and self.hist_cap) else (None, 0)
-        _lib.call("qsc_scpass_loop", self.desc, _lib.ptr(self.s_entries),
-                  _lib.ptr(o.s_width), _lib.ptr(o.s_off), _lib.ptr(self.c_entries),
-                  _lib.ptr(o.c_width), _lib.ptr(o.c_off), _lib.ptr(o.c_kmap), o.model, self.R,
-                  _lib.ptr(S_pos), _lib.ptr(C), _lib.ptr(mS), _lib.ptr(vS), adam_s,
-                  float(lambda_s), _lib.ptr(mC), _lib.ptr(vC), adam_c, float(lambda_c),
-                  _lib.ptr(self.state), _lib.ptr(hist), cap, int(n), _lib.ptr(self.ws),
-                  self.ws.numel(), _lib.stream())
-
-    def loop_counters(self):
-        """(arrivals, completed groups) counted by the last persistent-loop launch on this
-        engine's workspace (diagnostics; synchronises)."""
-        off = int(_lib.lib().qsc_pass_sync_offset(self.desc, self.R))
-        if off < 0:
-            raise _lib.QscError("qsc_pass_sync_offset failed")
-        # uint64 words (include/qsc.h): 16 g group arrivals (g < 16), 256 completed groups
-        w = self.ws[off:off + 272 * 8].cpu().view(torch.int64)
-        return int(w[0:256:16].sum().item()), int(w[256].item())
-
     def supdate(self, S_pos, mS, vS, g, adam, lambda_s):
         _lib.call("qsc_supdate", self.desc, self.R, _lib.ptr(S_pos), _lib.ptr(mS), _lib.ptr(vS),
                   _lib.ptr(g), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),

@@ -14,7 +14,6 @@ loop at :559-645); qmc/qmc.py is only its import preamble.  Per outer iteration 
     reference's GAN path, Z optimised, network frozen: :547-550).
 """
 import math
-import os
 import warnings
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -38,7 +37,6 @@ class SolveResult:
     Z: Optional[torch.Tensor] = None
     iters: int = 0
     fused: bool = False                 # S-step + next C-pass ran as one launch (qsc_scpass)
-    loop: bool = False                  # ... all in one persistent launch (qsc_scpass_loop)
 
 
 # Longest run captured as one hipGraph; longer runs replay several (results are identical:
@@ -52,11 +50,8 @@ def issue_iterations(solver, n):
     finish): c_step, fused_body x (n-1), s_step -- two launches per iteration."""
     if getattr(solver, "fuse", False) and n >= 2:
         solver.c_step()
-        if getattr(solver, "loop", False):
-            solver.fused_loop(n - 1)  # the n - 1 fused bodies in one persistent launch
-        else:
-            for _ in range(n - 1):
-                solver.fused_body()
+        for _ in range(n - 1):
+            solver.fused_body()
         solver.s_step()
     else:
         for _ in range(n):
@@ -227,7 +222,7 @@ class FreeSSolver:
 
     def __init__(self, obs, S_init, C_init, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
                  betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024, fuse=True,
-                 T_true=None, nmse_every=0, project_s=False, loop=None):
+                 T_true=None, nmse_every=0, project_s=False):
         self.obs = obs
         R = S_init.shape[0]
         self.R = R
@@ -256,16 +251,6 @@ class FreeSSolver:
                                           dtype=torch.float64, device=self.S.device)
             self._nmse_ws = torch.empty(_lib.lib().qsc_reduce_workspace_bytes(0),
                                         dtype=torch.uint8, device=self.S.device)
-        # the fused bodies of a run in ONE persistent launch (qsc_scpass_loop: every tile's
-        # workgroup resident, the C-step finish split over the tile groups and every
-        # workgroup's head; bit-exact with the launch pairs); not with per-iteration NMSE
-        # tracking, which runs between an S-step and the next finish.  loop=None: QSC_LOOP
-        # (default on); loop=True/False forces it on/off where supported
-        if loop is None:
-            loop = os.environ.get("QSC_LOOP", "1") == "1"
-        self.loop = (self.fuse and bool(loop) and not self.nmse_every
-                     and self.engine.scpass_loop_supported())
-
     # one outer iteration = C grad-step + S grad-step
     def c_step(self):
         e = self.engine
@@ -286,14 +271,6 @@ class FreeSSolver:
         e = self.engine
         e.scpass(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s)
         self._track()  # (S_{i+1}, C_{i+1}): C is updated by the cfinish below
-        e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)
-
-    def fused_loop(self, n):
-        """n fused bodies (fused_body x n, bit for bit) as one persistent launch and the last
-        body's C-step finish (qsc_scpass_loop, then qsc_cfinish)."""
-        e = self.engine
-        e.scpass_loop(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s, self.mC,
-                      self.vC, self.adam_c, self.lambda_c, n)
         e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)
 
     def _track(self):
@@ -324,8 +301,7 @@ class FreeSSolver:
         prepare_iterations(self, n)
 
     def run(self, n, use_graph=False):
-        """Enqueue n outer iterations (no host sync).  With `loop`, read results through
-        S_pixels() / history() or call check(): they raise if a persistent-loop wait timed out."""
+        """Enqueue n outer iterations (no host sync)."""
         run_iterations(self, n, use_graph)
 
     # ---- results --------------------------------------------------------------------------
@@ -333,20 +309,10 @@ class FreeSSolver:
         return self.engine.read_state()
 
     def S_pixels(self):
-        if self.loop:
-            self.check()  # one small readback: a timed-out loop wait leaves C incomplete
         return self.obs.to_pixels(self.S, self.R).reshape(self.R, 1, self.obs.I, self.obs.J)
-
-    def check(self):
-        """Raise if a persistent-loop launch of this solver timed out waiting for the other
-        tiles (the run's C updates are then incomplete, include/qsc.h qsc_scpass_loop)."""
-        if self.state().get("fused_fault"):
-            raise _lib.QscError("qsc_scpass_loop: a wait timed out; rerun with loop=False / "
-                                "QSC_LOOP=0")
 
     def history(self):
         self.engine.flush()  # settle the last S-pass (its history row)
-        self.check()
         st = self.state()
         n = min(int(st["iter"]), self.engine.hist_cap)
         h = self.engine.hist[: 4 * n].view(n, 4).double().cpu()
@@ -365,7 +331,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
           betas=(0.9, 0.999), eps=1e-8, project_c=True, generator=None, Z_init=None,
           restart=False, restart_samples=(200, 200), T_true=None, nmse_every=0,
           use_graph=False, obs=None, tile=None, callback=None, loss="probit", fuse=True,
-          loop=None, project_s=False):
+          project_s=False):
     """Alternating S/C probit-MLE (qmc/qmc.ipynb :559-645).
 
     Args mirror the notebook globals: Y (K,1,I,J) bin indices, Wx (K,1,I,J) 0/1 mask,
@@ -402,7 +368,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
         sol = FreeSSolver(obs, S_init, C_init, lambda_c, lambda_s, lr_c, lr_s, betas, eps,
                           project_c, hist_cap=max_iter, fuse=fuse,
                           T_true=T_true if nmse_every else None, nmse_every=nmse_every,
-                          loop=loop, project_s=project_s)
+                          project_s=project_s)
         done = 0
         chunk = nmse_every if (callback is not None and nmse_every) else max_iter
         while done < max_iter:
@@ -414,8 +380,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
         nmse = sol.nmse_history()
         costs_c, costs_s = sol.history()
         return SolveResult(S=sol.S_pixels(), C=sol.C.clone(), costs_c=costs_c, costs_s=costs_s,
-                           nmse=nmse, iters=max_iter, fused=sol.fuse,
-                           loop=sol.loop and max_iter >= 2)
+                           nmse=nmse, iters=max_iter, fused=sol.fuse)
     return _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c, lr_s,
                             max_iter, betas, eps, project_c, restart, restart_samples, T_true,
                             nmse_every, callback)

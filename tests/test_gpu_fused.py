@@ -592,50 +592,13 @@ def test_phase_split_fused_launch_is_bitexact():
     assert a.costs_c == b.costs_c and a.costs_s == b.costs_s
 
 
-@pytest.mark.parametrize("n", [2, 3, 11])
-@pytest.mark.parametrize("shape", [(8, 192, 192, 256, 1024),  # 36 tiles: ragged tile groups
-                                   (8, 384, 384, 256, 1024),  # 144 tiles
-                                   (4, 128, 128, 64, 1024),   # 16 tiles: one per group
-                                   (4, 96, 96, 64, 1024),     # 9 tiles: fewer than 16 groups
-                                   (4, 128, 128, 64, 128),    # 4-wave workgroups
-                                   (4, 256, 256, 64, 256),    # 8 waves (C2 class)
-                                   (3, 96, 96, 70, 384)])     # 12 waves, two ragged k-slices
-def test_persistent_loop_is_bitexact(n, shape):
-    """qsc_scpass_loop (the n - 1 fused bodies in ONE persistent launch: the C-step finish split
-    over the tile groups' last arrivals and every workgroup's head, include/qsc.h) then the last
-    qsc_cfinish give the launch pairs' S, C, moments, history and state bit for bit, eager and
-    hipGraph, with every counter where it should be (each tile's arrival and each group's
-    record, every body)."""
-    from quantized_spectrum_cartography_amd.obs import Observations
-    from quantized_spectrum_cartography_amd.qmc import FreeSSolver
-    R, I, J, K, tile = shape
-    d = _random_case(58, R, I, J, K)
-    o = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=R, tile=tile)
-    ref = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, loop=False)
-    assert ref.fuse and not ref.loop
-    ref.run(n)
-    nt = o.desc.ntiles
-    for g in (False, True):
-        sol = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, loop=True)
-        assert sol.loop, "the persistent loop does not apply at this shape"
-        sol.run(n, use_graph=g)
-        for x, y in ((ref.S, sol.S), (ref.C, sol.C), (ref.mS, sol.mS), (ref.vS, sol.vS),
-                     (ref.mC, sol.mC), (ref.vC, sol.vC)):
-            assert torch.equal(x, y)
-        assert ref.history() == sol.history()
-        st, rs = sol.state(), ref.state()
-        assert st["fused_fault"] == 0
-        assert st == rs
-        assert sol.engine.loop_counters() == ((n - 1) * nt, (n - 1) * min(nt, 16))
-
-
 @pytest.mark.parametrize("log_model,R,I,J,K,s_scale,lr_s,n", [
     (True, 4, 32, 32, 16, None, 0.1, 3),        # log model: 0.5 % of S projected
     (False, 8, 64, 64, 256, 0.02, 0.05, 6)])   # one-bit, fused launches
 def test_project_s_matches_reference_op_sequence(log_model, R, I, J, K, s_scale, lr_s, n):
     """project_s (S[S<0] = 0 after each S-step, fused into the S-side Adam of the pass kernels;
     the log model's S >= 0 domain) vs the oracle's op sequence with the same projection, on a
-    start where the unprojected S goes negative -- through the fused launches (the loop included)
+    start where the unprojected S goes negative -- through the fused launches
     for the one-bit case, the three-launch form for the log model."""
     from quantized_spectrum_cartography_amd import qmc
     d = _random_case(61, R, I, J, K, f=0.3, log_model=log_model)

@@ -50,6 +50,11 @@ def main():
     print("  start      ", pu(st[:, 28] - r0))
     print("  end        ", pu(st[:, 29] - r0))
     print("  staging    ", pc(st[:, 1] - st[:, 0]))
+    w = np.arange(len(st)) % 16  # wave in workgroup (rows are wg-major: tile * 16 + wave)
+    for nm, m in (("early", w < 4), ("late", w >= 4)):
+        print("   %-5s C^T rows written" % nm, pc(st[m, 10] - st[m, 0]))
+        print("   %-5s barrier passed  " % nm, pc(st[m, 1] - st[m, 10]))
+    print("  start->C^T (realtime, vs grid start)", pu(st[:, 28] - r0 + (st[:, 10] - st[:, 0]) / ghz * 0.1))
     if (st[:, 12] > 0).any():
         m = st[:, 12] > 0
         print("  1st data   ", pc(st[m, 12] - st[m, 1]))
