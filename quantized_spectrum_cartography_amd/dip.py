@@ -74,7 +74,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R, offset=None, log_model=True, deco
           Z_init=None, C_init=None, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
           max_iter=500, optimize="weights", T_true=None, nmse_every=0, obs=None, tile=None,
           seed=0, callback=None, S_init=None, prefit_steps=1000, prefit_lr=1e-2, ndf=16,
-          warm="residual", residual_scale=None):
+          warm="residual", residual_scale=None, lr_c_rel=1e-2, calibrate=True):
     """DIP-regularised alternating probit MLE (config 5: log model + DIP prior on S).
 
     `offset` defaults to the reference log model's LOG_OFFSET_7_ADJUSTED
@@ -93,7 +93,18 @@ def solve(Y, Wx, bin_boundaries, noise_std, R, offset=None, log_model=True, deco
       warm="prefit": the decoder itself is pre-fitted to S_init (`prefit_steps` Adam steps at
         `prefit_lr`) and C_init rescaled by the pre-fit's field scale (a 256 x 256 decoder of
         the reference's widths cannot reproduce the fields' peaks: profiles/r04/c5_explore*).
-    A fresh decoder is always BN-calibrated (calibrate_bn)."""
+    calibrate=True (default since round 4): a decoder built here is BN-calibrated at Z_init
+    (calibrate_bn) -- a data-dependent initialisation the reference does not have (its DIP
+    notebook is not shipped), so the cold-start numbers differ from an uncalibrated decoder's
+    (parity unpinned); calibrate=False keeps the fresh BatchNorm statistics.
+
+    lr_c="auto": the C-step's Adam step sized to the data instead of the notebook's absolute 5e-3
+    (qmc/qmc.ipynb :549), which assumes maps of unit scale: lr_c = lr_c_rel x c_target with
+    c_target = mean(T_hat) / (R mean(S_start)), T_hat the de-quantized map (warm.dequantize) and
+    S_start the S the solve starts from -- so from the notebook's zero C the C-step reaches the
+    data's scale in ~1/lr_c_rel steps instead of overshooting it by orders of magnitude (a
+    generated C5 map has T ~ 1e-5: at 5e-3 the cold start oscillates to map NMSE ~4, profiles/r04/
+    quality.json).  The value used is returned as result.lr_c."""
     if log_model:
         offset = LOG_OFFSET if offset is None else float(offset)
         if not offset > 0.0:
@@ -113,7 +124,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R, offset=None, log_model=True, deco
         Z_init = torch.randn((R, 256), generator=g)
     if C_init is None:
         C_init = torch.zeros(R, K)
-    if fresh:
+    if fresh and calibrate:
         calibrate_bn(decoder, Z_init.detach().to(dev, torch.float32))
     net = decoder
     if S_init is not None and warm == "prefit":
@@ -140,11 +151,30 @@ def solve(Y, Wx, bin_boundaries, noise_std, R, offset=None, log_model=True, deco
     if optimize in ("weights", "both"):
         params += list(decoder.parameters())
     Zp = Z_init.detach().to(dev, torch.float32).clone()
+    if isinstance(lr_c, str):
+        if lr_c != "auto":
+            raise ValueError("lr_c must be a number or 'auto'")
+        with torch.no_grad():
+            s_mean = float(net(Zp).abs().mean())
+        lr_c = float(lr_c_rel) * _c_target(Y, Wx, bin_boundaries, noise_std, R, s_mean,
+                                            offset if log_model else 0.0, log_model)
     res = _solve_generator(obs, net, Zp, C_init, R, lambda_c, lambda_s, lr_c, lr_s, max_iter,
                            (0.9, 0.999), 1e-8, True, False, (0, 0), T_true, nmse_every, callback,
                            params=params, optimize_z=optimize in ("z", "both"))
     res.decoder = decoder
+    res.lr_c = float(lr_c)
     return res
+
+
+def _c_target(Y, Wx, bin_boundaries, noise_std, R, s_mean, offset, log_model):
+    """mean(T_hat) / (R s_mean): the magnitude of C at which T_hat = S C has the de-quantized
+    data's scale (dip.solve lr_c="auto")."""
+    from .warm import dequantize
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    xh = dequantize(Y.to(dev), Wx.to(dev) if Wx is not None else None, bin_boundaries,
+                    noise_std)
+    t = (torch.exp(xh) - float(offset)).clamp_min(0.0) if log_model else xh.clamp_min(0.0)
+    return float(t.mean()) / (R * max(s_mean, 1e-30))
 
 
 class _Residual(torch.nn.Module):
