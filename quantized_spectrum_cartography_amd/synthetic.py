@@ -299,6 +299,11 @@ CONFIGS = {
     # one GPU's K-slab share of c4 at N = 8 (K_loc = 1024 / 8): the per-GPU kernel of the
     # north-star 8-GPU layout, benchable on one GPU
     "c4k": (512, 512, 128, 16),
+    # one GPU's K-slab share of c3 at N = 2, 4, 8 (K_loc = 256 / N): the per-GPU sequence of
+    # the default strong K-slab bench line, for the 1 -> 8 projection of DESIGN.md section 5
+    "c3k2": (512, 512, 128, 8),
+    "c3k4": (512, 512, 64, 8),
+    "c3k8": (512, 512, 32, 8),
     # log model (4 log bins, sigma 5) on a generated map, free S (c5_problem)
     "c5": (256, 256, 64, 4),
 }
