@@ -54,7 +54,7 @@ constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 #endif
 // fused launch: waves that read their first slice before the staging barrier (see scfused)
 #ifndef QSC_EARLY_WAVES
-#define QSC_EARLY_WAVES 4
+#define QSC_EARLY_WAVES 16
 #endif
 // fused launch: a wave's first slice lands before its second slice's reads are issued
 #ifndef QSC_FIRST_WAIT
@@ -1580,10 +1580,12 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   int il = local_of(0);
   SliceIn<RP, E, ADAM> cur;
   const SliceLane ln = slice_lane<RP, E>(p, h);
-  // Staggered first reads: a SIMD runs its waves nearly one after another (oldest first), so
-  // only the oldest wave of each SIMD (w < QSC_EARLY_WAVES) reads its first slice now; the
-  // others read theirs after the staging barrier, while the oldest ones compute.  The first
-  // burst is then a quarter of the tile's slice data and the S-step starts that much earlier.
+  // First reads before the staging: waves w < QSC_EARLY_WAVES read their first slice now, the
+  // others after the staging barrier.  The C^T reads the staging waits for take 2.5-3 us at a
+  // launch's start (profiles/r05/stamps_f.log), long enough to cover every wave's first slice:
+  // with all 16 waves early the fused launch is 0.6-0.9 us shorter at C3 than with the oldest
+  // wave of each SIMD only (QSC_EARLY_WAVES=4, round 3's choice when the staging was shorter;
+  // profiles/r05/ab_early_waves.log).
   const bool early = w < QSC_EARLY_WAVES;
   auto stage = [&]() {
 #if QSC_CT_VEC

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--cold-lr-c", nargs="*", default=["5e-3", "auto"])
     ap.add_argument("--cold-lr-s", type=float, nargs="*", default=[1e-2])
+    ap.add_argument("--cold-lr-c-rel", type=float, nargs="*", default=[1e-2])
     ap.add_argument("--warm-forms", nargs="*", default=["relative"])
     ap.add_argument("--warm-lr-s", type=float, nargs="*", default=[3e-2])
     ap.add_argument("--warm-lr-c-scale", type=float, nargs="*", default=[1e-2])
@@ -69,8 +70,12 @@ def main():
     c_mag = float(C0.abs().mean())
     for lr_c in args.cold_lr_c:
         for lr_s in args.cold_lr_s:
-            run("cold_lrc%s_lrs%g" % (lr_c, lr_s),
-                lr_c=(lr_c if lr_c == "auto" else float(lr_c)), lr_s=lr_s)
+            for rel in (args.cold_lr_c_rel if lr_c == "auto" else [None]):
+                kw = dict(lr_c=(lr_c if lr_c == "auto" else float(lr_c)), lr_s=lr_s)
+                if rel is not None:
+                    kw["lr_c_rel"] = rel
+                run("cold_lrc%s%s_lrs%g" % (lr_c, "" if rel is None else "_rel%g" % rel, lr_s),
+                    **kw)
     for form in args.warm_forms:
         for lr_s in args.warm_lr_s:
             for cs in args.warm_lr_c_scale:
