@@ -13,10 +13,12 @@ Prints one JSON line of trajectories (map NMSE every few iterations, qmc/quantiz
               FFT-correlated log-normal shadowing, 256 x 256, K = 64, R = 4) quantized with the log
               model as qmc/qmc.ipynb :537 does (4 log bins, LOG_OFFSET_4, sigma = 5), f = 0.1:
                 c5_warm_start  the de-quantized SPA warm start (warm.warm_start);
-                c5_dip       the DIP solver from it (dip.solve warm="relative": S = S0
-                             exp(D(Z) - D(Z0)), decoder weights optimised, C from C0);
+                c5_dip       the DIP solver from it (dip.solve warm="residual": S = max(S0 +
+                             a (D(Z) - D(Z0)), 0), decoder weights optimised, C from C0; the
+                             step sizes of tools/c5_dip_sweep.py's best point, profiles/r05/
+                             c5_dip_sweep_*.log);
                 c5_dip_cold  the DIP solver from zero C (BN-calibrated decoder), the notebook's
-                             cold setting;
+                             cold setting, with the C-step sized to the data (lr_c="auto");
                 c5_free_warm_projS_*  free S >= 0 (project_s) from the warm start.
 
   python tools/quality.py [--c2-iters 4000] [--dip-iters 600]
@@ -46,7 +48,9 @@ def main():
     ap.add_argument("--warm-width", type=float, default=8.0)
     ap.add_argument("--warm-lr-s", type=float, default=1e-3)
     ap.add_argument("--dip-warm-iters", type=int, default=3000)
-    ap.add_argument("--dip-lr-s", type=float, default=0.03)
+    ap.add_argument("--dip-lr-s", type=float, default=0.01)
+    ap.add_argument("--dip-form", default="residual", choices=["residual", "relative"])
+    ap.add_argument("--dip-cold-lr-c", default="auto")
     ap.add_argument("--dip-lr-c-scale", type=float, default=1e-2)
     ap.add_argument("--free-lr-scales", type=float, nargs="*", default=[1e-2, 1e-3])
     ap.add_argument("--skip-c2", action="store_true")
@@ -93,10 +97,13 @@ def main():
         every = max(1, args.dip_iters // 12)
         t0 = time.perf_counter()
         rd = dip.solve(Y, Wx, b, 5.0, R, offset=LOG_OFFSET_4, max_iter=args.dip_iters,
-                       T_true=T, nmse_every=every)
+                       T_true=T, nmse_every=every,
+                       lr_c=(args.dip_cold_lr_c if args.dip_cold_lr_c == "auto"
+                             else float(args.dip_cold_lr_c)))
         torch.cuda.synchronize()
         zero = float(metrics.map_nmse(torch.zeros_like(rd.S), rd.C, T, log_offset=LOG_OFFSET_4))
         out["c5_dip_cold"] = {"iters": args.dip_iters, "wall_s": time.perf_counter() - t0,
+                              "lr_c": rd.lr_c, "finite": bool(torch.isfinite(rd.S).all()),
                               "map_nmse": traj(rd, every), "slf_nmse": metrics.slf_nmse(rd.S, S_true),
                               # NMSE_LOG (qmc/quantization_model_log.py:104-111): the log-domain
                               # error the log model is fitted in, vs the all-zero map's
@@ -133,20 +140,22 @@ def c5_warm_runs(Y, Wx, b, T, S_true, R, args):
                             "wall_s": time.perf_counter() - t0}
     print(json.dumps({"c5_warm_start": [lin, lg]}), file=sys.stderr, flush=True)
     s_mag, c_mag = float(S0.abs().mean()), float(C0.abs().mean())
-    # c5_dip: the DIP solver from the warm start (dip.solve warm="relative": S = S0 exp(D(Z) -
-    # D(Z0)), the decoder's weights optimised; C from C0), Adam steps at the warm-start C's
-    # scale for C and lr_s for the decoder weights
+    # c5_dip: the DIP solver from the warm start (dip.solve warm=args.dip_form, the decoder's
+    # weights optimised; C from C0), Adam steps at the warm-start C's scale for C and lr_s for
+    # the decoder weights
     every = 25
     t0 = time.perf_counter()
     rd = dip.solve(Y, Wx, b, 5.0, R, offset=LOG_OFFSET_4, max_iter=args.dip_warm_iters,
                    S_init=S0.cpu(), C_init=C0.cpu(), lr_c=args.dip_lr_c_scale * c_mag,
-                   lr_s=args.dip_lr_s, warm="relative", T_true=T, nmse_every=every,
+                   lr_s=args.dip_lr_s, warm=args.dip_form, T_true=T, nmse_every=every,
                    seed=args.seed)
     torch.cuda.synchronize()
     lin_f, lg_f = _nmse_pair(rd.S, rd.C, T, LOG_OFFSET_4)
     tr = traj(rd, every)
     out["c5_dip"] = {"iters": args.dip_warm_iters, "start": "warm (c5_warm_start)",
-                     "form": "relative: S = S0 exp(D(Z) - D(Z0))", "lr_s": args.dip_lr_s,
+                     "form": ("relative: S = S0 exp(D(Z) - D(Z0))" if args.dip_form == "relative"
+                              else "residual: S = max(S0 + a (D(Z) - D(Z0)), 0)"),
+                     "lr_s": args.dip_lr_s,
                      "lr_c": args.dip_lr_c_scale * c_mag,
                      "map_nmse": tr[:: max(1, len(tr) // 12)],
                      "map_nmse_best": min(tr, key=lambda x: x[1]) if tr else None,
