@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--warm-lr-s", type=float, nargs="*", default=[3e-2])
     ap.add_argument("--warm-lr-c-scale", type=float, nargs="*", default=[1e-2])
     ap.add_argument("--lambda-s", type=float, default=100.0)
+    ap.add_argument("--refine", type=int, nargs="*", default=[0])
+    ap.add_argument("--seeds", type=int, nargs="*", default=[None])
     args = ap.parse_args()
     from quantized_spectrum_cartography_amd import dip, maps, metrics, warm
     from quantized_spectrum_cartography_amd import quantization_model_log as qml
@@ -47,15 +49,16 @@ def main():
                     slf=round(metrics.slf_nmse(S, S_true), 5),
                     finite=bool(torch.isfinite(S).all() and torch.isfinite(C).all()))
 
-    def run(name, **kw):
+    def run(name, seed=None, **kw):
         path = []
 
         def cb(i, d):
             if i % args.every == 0:
                 path.append([i, metrics_of(d["S"].detach(), d["C"])])
         t0 = time.perf_counter()
-        res = dip.solve(Y, Wx, b, 5.0, R, offset=off, max_iter=args.iters, seed=args.seed,
-                        callback=cb, lambda_s=args.lambda_s, **kw)
+        res = dip.solve(Y, Wx, b, 5.0, R, offset=off, max_iter=args.iters,
+                        seed=args.seed if seed is None else seed, callback=cb,
+                        lambda_s=args.lambda_s, **kw)
         torch.cuda.synchronize()
         out = {"kw": {k: (v if isinstance(v, (int, float, str)) else "tensor")
                       for k, v in kw.items()},
@@ -64,9 +67,14 @@ def main():
                "wall_s": round(time.perf_counter() - t0, 2)}
         print(json.dumps({name: out}), flush=True)
 
-    S0, C0 = warm.warm_start(Y.cuda(), Wx.cuda(), b, 5.0, R, offset=off, log_model=True, width=8.0)
-    torch.cuda.synchronize()
-    print(json.dumps({"warm_start": metrics_of(S0, C0)}), flush=True)
+    starts = {}
+    for rf in args.refine:
+        S0, C0 = warm.warm_start(Y.cuda(), Wx.cuda(), b, 5.0, R, offset=off, log_model=True,
+                                 width=8.0, refine=rf)
+        torch.cuda.synchronize()
+        starts[rf] = (S0, C0)
+        print(json.dumps({"warm_start_refine%d" % rf: metrics_of(S0, C0)}), flush=True)
+    S0, C0 = starts[args.refine[0]]
     c_mag = float(C0.abs().mean())
     for lr_c in args.cold_lr_c:
         for lr_s in args.cold_lr_s:
@@ -76,11 +84,15 @@ def main():
                     kw["lr_c_rel"] = rel
                 run("cold_lrc%s%s_lrs%g" % (lr_c, "" if rel is None else "_rel%g" % rel, lr_s),
                     **kw)
-    for form in args.warm_forms:
-        for lr_s in args.warm_lr_s:
-            for cs in args.warm_lr_c_scale:
-                run("warm_%s_lrs%g_lrc%g" % (form, lr_s, cs), S_init=S0.cpu(), C_init=C0.cpu(),
-                    lr_c=cs * c_mag, lr_s=lr_s, warm=form)
+    for rf, (S0, C0) in starts.items():
+        c_mag = float(C0.abs().mean())
+        for form in args.warm_forms:
+            for lr_s in args.warm_lr_s:
+                for cs in args.warm_lr_c_scale:
+                    for sd in args.seeds:
+                        run("warm_rf%d_%s_lrs%g_lrc%g_seed%s" % (rf, form, lr_s, cs, sd),
+                            seed=sd, S_init=S0.cpu(), C_init=C0.cpu(), lr_c=cs * c_mag,
+                            lr_s=lr_s, warm=form)
 
 
 if __name__ == "__main__":
