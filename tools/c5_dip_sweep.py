@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--lambda-s", type=float, default=100.0)
     ap.add_argument("--refine", type=int, nargs="*", default=[0])
     ap.add_argument("--seeds", type=int, nargs="*", default=[None])
+    ap.add_argument("--residual-scale-rel", type=float, nargs="*", default=[1.0],
+                    help="dip.solve residual_scale as a multiple of its default")
     args = ap.parse_args()
     from quantized_spectrum_cartography_amd import dip, maps, metrics, warm
     from quantized_spectrum_cartography_amd import quantization_model_log as qml
@@ -90,9 +92,12 @@ def main():
             for lr_s in args.warm_lr_s:
                 for cs in args.warm_lr_c_scale:
                     for sd in args.seeds:
-                        run("warm_rf%d_%s_lrs%g_lrc%g_seed%s" % (rf, form, lr_s, cs, sd),
-                            seed=sd, S_init=S0.cpu(), C_init=C0.cpu(), lr_c=cs * c_mag,
-                            lr_s=lr_s, warm=form)
+                        for ar in args.residual_scale_rel:
+                            a0 = float(S0.abs().mean()) if form == "residual" else 1.0
+                            run("warm_rf%d_%s_lrs%g_lrc%g_a%g_seed%s" % (rf, form, lr_s, cs, ar,
+                                                                        sd),
+                                seed=sd, S_init=S0.cpu(), C_init=C0.cpu(), lr_c=cs * c_mag,
+                                lr_s=lr_s, warm=form, residual_scale=ar * a0)
 
 
 if __name__ == "__main__":
