@@ -65,6 +65,8 @@ def main():
         out = {"kw": {k: (v if isinstance(v, (int, float, str)) else "tensor")
                       for k, v in kw.items()},
                "final": metrics_of(res.S, res.C), "path": path,
+               "cost_first": res.costs_s[0], "cost_last": res.costs_s[-1],
+               "nll_c_last": res.costs_c[-1],
                "lr_c_used": getattr(res, "lr_c", None),
                "wall_s": round(time.perf_counter() - t0, 2)}
         print(json.dumps({name: out}), flush=True)
