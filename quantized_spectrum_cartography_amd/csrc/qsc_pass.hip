@@ -56,6 +56,11 @@ constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 #ifndef QSC_EARLY_WAVES
 #define QSC_EARLY_WAVES 16
 #endif
+// fused launch: the other waves read their first slice right after their staging (1) or after
+// the staging barrier (0)
+#ifndef QSC_LATE_LOADS
+#define QSC_LATE_LOADS 0
+#endif
 // fused launch: a wave's first slice lands before its second slice's reads are issued
 #ifndef QSC_FIRST_WAIT
 #define QSC_FIRST_WAIT 1
@@ -1664,9 +1669,17 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     stage();
   } else {
     stage();
+#if QSC_LATE_LOADS
+    // (after this wave's C^T reads have landed -- the staging waited for them -- so they are
+    // not queued behind the late waves' slice data; before the barrier, so that data streams
+    // in while the oldest waves compute)
+    slice_load(cur, s_ent, s_width, s_off, global_of(il < nsl ? il : 0), ln, S, mS, vS);
+#endif
   }
   __syncthreads();
+#if !QSC_LATE_LOADS
   if (!early) slice_load(cur, s_ent, s_width, s_off, global_of(il < nsl ? il : 0), ln, S, mS, vS);
+#endif
   STAMP(wg, 1);
   if (t == 0) {
     // ||C_i||^2 for the next C update's regulariser, from the staged C^T at the start (as a
