@@ -332,6 +332,59 @@ def test_dip_solver_256():
     assert np.all(np.isfinite(res.costs_c))
 
 
+def test_dip_auto_lr_c_sizes_the_c_step_to_the_data():
+    """dip.solve(lr_c="auto") from the notebook's zero C: lr_c = lr_c_rel x mean(T_hat) / (R
+    mean(S_start)) with T_hat the de-quantized map (dip._c_target); on a map of scale ~1e-4 the
+    notebook's absolute 5e-3 overshoots by orders of magnitude (round 4's C5 cold run, map NMSE
+    4.1), the auto step keeps the map NMSE below the all-zero map's ~1 and everything finite."""
+    from quantized_spectrum_cartography_amd import dip, metrics, warm
+    from quantized_spectrum_cartography_amd.utils import QUANTIZATION_BOUNDARIES_4_BINS_LOG
+    torch.manual_seed(3)
+    R, K, N = 2, 8, 64
+    S_true = torch.rand(R, 1, N, N) * 2e-4
+    C_true = torch.rand(R, K)
+    Tt = ro.get_tensor(S_true, C_true)
+    b = torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG)
+    Y = ro.quantize(Tt, 5.0, b, offset=1e-10, log_model=True).unsqueeze(1)
+    Wx = torch.bernoulli(torch.full((K, 1, N, N), 0.1))
+    res = dip.solve(Y, Wx, b, 5.0, R, offset=1e-10, max_iter=40, lr_c="auto")
+    xh = warm.dequantize(Y.cuda(), Wx.cuda(), b, 5.0)
+    t_mean = float((torch.exp(xh) - 1e-10).clamp_min(0.0).mean())
+    assert 0.0 < res.lr_c < 1e-3 * 5e-3 / 1e-4  # orders of magnitude below the notebook's step
+    # (the decoder's sigmoid output averages between 0.01 and 1 at the start)
+    assert 1e-2 * t_mean / R <= res.lr_c <= t_mean / R
+    assert np.all(np.isfinite(res.costs_c)) and np.all(np.isfinite(res.costs_s))
+    T = Tt.reshape(K, N, N).cuda()
+    assert float(metrics.map_nmse(res.S, res.C, T)) < 1.5
+    with pytest.raises(ValueError):
+        dip.solve(Y, Wx, b, 5.0, R, offset=1e-10, max_iter=1, lr_c="fast")
+
+
+def test_warm_start_refine_keeps_the_factorisation():
+    """warm.warm_start(refine=n): the ANLS sweeps keep S, C >= 0 and do not raise the linear
+    fit residual ||C^T S - T_hat|| of the SPA start (each sweep solves a non-negative least
+    squares in one factor with the other fixed)."""
+    from quantized_spectrum_cartography_amd import warm
+    from quantized_spectrum_cartography_amd.utils import QUANTIZATION_BOUNDARIES_4_BINS_LOG
+    torch.manual_seed(4)
+    R, K, N = 3, 16, 48
+    S_true = torch.rand(R, 1, N, N) ** 3
+    C_true = torch.rand(R, K)
+    Tt = ro.get_tensor(S_true, C_true)
+    b = torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG)
+    Y = ro.quantize(Tt, 1.0, b, offset=1e-10, log_model=True).unsqueeze(1).cuda()
+    Wx = torch.bernoulli(torch.full((K, 1, N, N), 0.3)).cuda()
+    xh = warm.dequantize(Y, Wx, b, 1.0)
+    Th = (torch.exp(xh) - 1e-10).clamp_min(0.0).reshape(K, -1)
+
+    def resid(S, C):
+        return float(torch.linalg.norm(C.t() @ S.reshape(R, -1) - Th))
+    S0, C0 = warm.warm_start(Y, Wx, b, 1.0, R, offset=1e-10, log_model=True)
+    S2, C2 = warm.warm_start(Y, Wx, b, 1.0, R, offset=1e-10, log_model=True, refine=2)
+    assert bool((S2 >= 0).all()) and bool((C2 >= 0).all())
+    assert resid(S2, C2) <= resid(S0, C0) * (1 + 1e-4)
+
+
 @pytest.mark.parametrize("warm", ["relative", "residual"])
 def test_dip_warm_start_forms(warm):
     """dip.solve from a warm start (S_init, C_init): the first S-step sees exactly the warm
