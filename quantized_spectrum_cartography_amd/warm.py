@@ -55,24 +55,11 @@ def dequantize(Y, Wx, bin_boundaries, noise_std, width=8.0, p_clip=0.02):
     return torch.stack(est).mean(0).to(dev)
 
 
-def warm_start(Y, Wx, bin_boundaries, noise_std, R, offset=0.0, log_model=False, width=8.0,
-               refine=0):
-    """(S0 (R, 1, I, J), C0 (R, K)) for qmc.solve / dip.solve from the quantized samples.
-
-    refine > 0: that many alternating non-negative least-squares sweeps on the de-quantized map
-    after SPA (S <- argmin_{S >= 0} ||C^T S - T_hat||, every pixel from all K bins instead of the
-    SPA's single picked bin per field; then C <- the same with S fixed), the ANLS refinement of
-    backup/algorithms/joint_opt_ae.m:404-417 on the MFMA Gram (gram.nnls_spectra)."""
+def warm_start(Y, Wx, bin_boundaries, noise_std, R, offset=0.0, log_model=False, width=8.0):
+    """(S0 (R, 1, I, J), C0 (R, K)) for qmc.solve / dip.solve from the quantized samples."""
     K = Y.shape[0]
     I, J = Y.shape[-2], Y.shape[-1]
     xh = dequantize(Y, Wx, bin_boundaries, noise_std, width)
     T = (torch.exp(xh) - float(offset)).clamp_min(0.0) if log_model else xh.clamp_min(0.0)
-    T = T.reshape(K, I * J)
-    C, S, sel = spa.spa_init(T, R)
-    if refine:
-        from . import gram
-        Tt = T.t().contiguous()
-        for _ in range(int(refine)):
-            S = gram.nnls_spectra(C, Tt)   # (R, P): per pixel, the K bins
-            C = gram.nnls_spectra(S, T)    # (R, K): per bin, the P pixels
+    C, S, sel = spa.spa_init(T.reshape(K, I * J), R)
     return S.reshape(R, 1, I, J), C

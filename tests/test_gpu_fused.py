@@ -360,31 +360,6 @@ def test_dip_auto_lr_c_sizes_the_c_step_to_the_data():
         dip.solve(Y, Wx, b, 5.0, R, offset=1e-10, max_iter=1, lr_c="fast")
 
 
-def test_warm_start_refine_keeps_the_factorisation():
-    """warm.warm_start(refine=n): the ANLS sweeps keep S, C >= 0 and do not raise the linear
-    fit residual ||C^T S - T_hat|| of the SPA start (each sweep solves a non-negative least
-    squares in one factor with the other fixed)."""
-    from quantized_spectrum_cartography_amd import warm
-    from quantized_spectrum_cartography_amd.utils import QUANTIZATION_BOUNDARIES_4_BINS_LOG
-    torch.manual_seed(4)
-    R, K, N = 3, 16, 48
-    S_true = torch.rand(R, 1, N, N) ** 3
-    C_true = torch.rand(R, K)
-    Tt = ro.get_tensor(S_true, C_true)
-    b = torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG)
-    Y = ro.quantize(Tt, 1.0, b, offset=1e-10, log_model=True).unsqueeze(1).cuda()
-    Wx = torch.bernoulli(torch.full((K, 1, N, N), 0.3)).cuda()
-    xh = warm.dequantize(Y, Wx, b, 1.0)
-    Th = (torch.exp(xh) - 1e-10).clamp_min(0.0).reshape(K, -1)
-
-    def resid(S, C):
-        return float(torch.linalg.norm(C.t() @ S.reshape(R, -1) - Th))
-    S0, C0 = warm.warm_start(Y, Wx, b, 1.0, R, offset=1e-10, log_model=True)
-    S2, C2 = warm.warm_start(Y, Wx, b, 1.0, R, offset=1e-10, log_model=True, refine=2)
-    assert bool((S2 >= 0).all()) and bool((C2 >= 0).all())
-    assert resid(S2, C2) <= resid(S0, C0) * (1 + 1e-4)
-
-
 @pytest.mark.parametrize("warm", ["relative", "residual"])
 def test_dip_warm_start_forms(warm):
     """dip.solve from a warm start (S_init, C_init): the first S-step sees exactly the warm

@@ -28,7 +28,6 @@ def main():
     ap.add_argument("--warm-lr-s", type=float, nargs="*", default=[3e-2])
     ap.add_argument("--warm-lr-c-scale", type=float, nargs="*", default=[1e-2])
     ap.add_argument("--lambda-s", type=float, default=100.0)
-    ap.add_argument("--refine", type=int, nargs="*", default=[0])
     ap.add_argument("--seeds", type=int, nargs="*", default=[None])
     ap.add_argument("--residual-scale-rel", type=float, nargs="*", default=[1.0],
                     help="dip.solve residual_scale as a multiple of its default")
@@ -71,14 +70,10 @@ def main():
                "wall_s": round(time.perf_counter() - t0, 2)}
         print(json.dumps({name: out}), flush=True)
 
-    starts = {}
-    for rf in args.refine:
-        S0, C0 = warm.warm_start(Y.cuda(), Wx.cuda(), b, 5.0, R, offset=off, log_model=True,
-                                 width=8.0, refine=rf)
-        torch.cuda.synchronize()
-        starts[rf] = (S0, C0)
-        print(json.dumps({"warm_start_refine%d" % rf: metrics_of(S0, C0)}), flush=True)
-    S0, C0 = starts[args.refine[0]]
+    S0, C0 = warm.warm_start(Y.cuda(), Wx.cuda(), b, 5.0, R, offset=off, log_model=True, width=8.0)
+    torch.cuda.synchronize()
+    starts = {0: (S0, C0)}
+    print(json.dumps({"warm_start": metrics_of(S0, C0)}), flush=True)
     c_mag = float(C0.abs().mean())
     for lr_c in args.cold_lr_c:
         for lr_s in args.cold_lr_s:
