@@ -61,6 +61,23 @@ constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 #ifndef QSC_LATE_LOADS
 #define QSC_LATE_LOADS 0
 #endif
+// fair wave priorities: a wave lowers its s_setprio level as it progresses (S-step: per slice;
+// C-pass walks: per quarter of the unit's chunk range), so the SIMD arbiter, oldest-first among
+// equal levels, keeps the waves of a SIMD abreast instead of finishing them one after another
+// (the last wave of a phase otherwise runs alone, latency-bound: profiles/r05/stamps_simd.log)
+#ifndef QSC_FAIR_PRIO
+#define QSC_FAIR_PRIO 0
+#endif
+__device__ __forceinline__ void prio_level(int lvl) {  // 3 = most urgent
+  if (lvl >= 3)
+    __builtin_amdgcn_s_setprio(3);
+  else if (lvl == 2)
+    __builtin_amdgcn_s_setprio(2);
+  else if (lvl == 1)
+    __builtin_amdgcn_s_setprio(1);
+  else
+    __builtin_amdgcn_s_setprio(0);
+}
 // fused launch: a wave's first slice lands before its second slice's reads are issued
 #ifndef QSC_FIRST_WAIT
 #define QSC_FIRST_WAIT 1
@@ -505,6 +522,12 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
                                             f2v (&acc)[RP / 2], f2v& nll) {
   using V4 = typename Ent<E>::V4;
   const int jlast = max(j1 - 1, 0);
+#if QSC_FAIR_PRIO
+  const int jfirst = jb, jspan = max(j1 - jb, 1);
+  auto fair = [&]() { prio_level(3 - min(3, (4 * (jb - jfirst)) / jspan)); };
+#else
+  auto fair = []() {};
+#endif
   if constexpr (PFC) {
   // software-pipelined gather: the LDS rows of the next entry pair are read before the current
   // pair's arithmetic, so the LDS latency runs under it (the group's chunks are loaded, clamped,
@@ -517,6 +540,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
     pair_rows<RP, E, KIND, 1>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
   }
   for (;;) {
+    fair();
     const int jn = jb + kGroup * js;
     const bool more = jn < j1;
     V4 nb[kGroup];
@@ -555,6 +579,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
   }
   } else {
   for (;;) {
+    fair();
     const int jn = jb + kGroup * js;
     const bool more = jn < j1;
     V4 nb[kGroup];
@@ -1703,6 +1728,9 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     const int il1 = local_of(n + 1);
     const bool more = il1 < nsl;
     const int s = global_of(il);
+#if QSC_FAIR_PRIO
+    prio_level(3 - min(3, n));  // (uniform: the wave's n-th slice)
+#endif
 #if QSC_FIRST_WAIT
     // the first slice's reads land before the second slice's are issued: the launch's first
     // burst is then one slice per wave, not two
