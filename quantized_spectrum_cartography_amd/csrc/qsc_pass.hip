@@ -61,12 +61,14 @@ constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 #ifndef QSC_LATE_LOADS
 #define QSC_LATE_LOADS 0
 #endif
-// fair wave priorities: a wave lowers its s_setprio level as it progresses (S-step: per slice;
-// C-pass walks: per quarter of the unit's chunk range), so the SIMD arbiter, oldest-first among
-// equal levels, keeps the waves of a SIMD abreast instead of finishing them one after another
-// (the last wave of a phase otherwise runs alone, latency-bound: profiles/r05/stamps_simd.log)
+// fair wave priorities: a wave lowers its s_setprio level as it progresses (S-step: per slice,
+// or with 2 per half slice; C-pass walks: per quarter of the unit's chunk range), so the SIMD
+// arbiter, oldest-first among equal levels, keeps the waves of a SIMD abreast instead of
+// finishing them one after another (the last wave of a phase otherwise runs alone,
+// latency-bound: profiles/r05/stamps_simd.log).  A/B at C3: fused launch -0.5 us
+// (profiles/r05/ab_fair_prio.log)
 #ifndef QSC_FAIR_PRIO
-#define QSC_FAIR_PRIO 0
+#define QSC_FAIR_PRIO 1
 #endif
 __device__ __forceinline__ void prio_level(int lvl) {  // 3 = most urgent
   if (lvl >= 3)
@@ -609,11 +611,16 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
                                             const f2v (&own)[RP / 2],
                                             const float* __restrict__ tab,
                                             const float2* __restrict__ edges, const Lik& lk,
-                                            f2v (&acc)[RP / 2], f2v& nll) {
+                                            f2v (&acc)[RP / 2], f2v& nll, int prio_top = -1) {
   using V2 = typename Ent<E>::V2;
   j1 = __builtin_amdgcn_readfirstlane(j1);
   const int jlast = max(j1 - 1, 0);
   int jb = 0;
+  // (QSC_FAIR_PRIO >= 2, prio_top >= 0: the wave's level drops from prio_top to prio_top - 1
+  // half-way through the slice)
+  auto fair = [&]() {
+    if (QSC_FAIR_PRIO >= 2 && prio_top >= 0) prio_level(prio_top - (2 * jb >= j1 ? 1 : 0));
+  };
   if constexpr (PF && is_sr(KIND)) {
     // software-pipelined gather (signed rows): the LDS rows of the next half chunk are read
     // before the current one's arithmetic, so the gather latency runs under it.  Every buffered
@@ -625,6 +632,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
       pair_rows<RP, E, KIND, 0>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
     }
     for (;;) {
+      fair();
       const int jn = jb + kGroupS;
       const bool more = jn < j1;
       V2 nb[kGroupS];
@@ -665,6 +673,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
     return;
   }
   for (;;) {
+    fair();
     const int jn = jb + kGroupS;
     const bool more = jn < j1;
     V2 nb[kGroupS];
@@ -1728,7 +1737,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     const int il1 = local_of(n + 1);
     const bool more = il1 < nsl;
     const int s = global_of(il);
-#if QSC_FAIR_PRIO
+#if QSC_FAIR_PRIO == 1
     prio_level(3 - min(3, n));  // (uniform: the wave's n-th slice)
 #endif
 #if QSC_FIRST_WAIT
@@ -1753,7 +1762,10 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     f2v nll = splat2(0.0f);
     walk_halves<RP, E, KIND, LOG, (QSC_ROW_PF_S != 0) && RP <= 8>(c.src, ln.ent, 2 * QSC_SLICE,
                                                                    c.j1, c.buf, own, Cl, El, lk,
-                                                                   accp, nll);
+                                                                   accp, nll,
+                                                                   QSC_FAIR_PRIO >= 2
+                                                                       ? max(3 - 2 * n, 1)
+                                                                       : -1);
     float acc[RP];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) {
