@@ -47,8 +47,24 @@ GRAPH_MAX_ITERS = 1024
 def issue_iterations(solver, n):
     """Kernel sequence of n outer iterations of a solver with c_step / s_step / iteration and,
     when `solver.fuse`, fused_body (S-step i + C-pass i+1 in one launch, then C-step i+1's
-    finish): c_step, fused_body x (n-1), s_step -- two launches per iteration."""
-    if getattr(solver, "fuse", False) and n >= 2:
+    finish): c_step, fused_body x (n-1), s_step -- two launches per iteration.
+
+    A solver with `chain` (FreeSSolver) ends a run with the fused launch instead of the
+    stand-alone S-step: its last S-step also runs the NEXT iteration's C-pass, whose partials
+    wait in the workspace (`ahead()`), and a following run starts with that C-pass's finish
+    instead of a C-pass of its own.  The op sequence of run(a) then run(b) is then exactly that
+    of run(a + b) -- c_step, fused_body x (a + b - 1), then the last S-step -- and every run of
+    n iterations issues n fused launches and n C-step finishes (the steady state), where the
+    stand-alone ends cost a C-pass and an S-pass per run."""
+    if getattr(solver, "fuse", False) and getattr(solver, "chain", False) and n >= 1:
+        if solver.ahead():
+            solver.c_finish()
+        else:
+            solver.c_step()
+        for _ in range(n - 1):
+            solver.fused_body()
+        solver.fused_last()
+    elif getattr(solver, "fuse", False) and n >= 2:
         solver.c_step()
         for _ in range(n - 1):
             solver.fused_body()
@@ -73,11 +89,14 @@ def _capture(solver, n, tolerant):
     s = capture_stream()
     caller = torch.cuda.current_stream()
     s.wait_stream(caller)
+    mark = solver.chain_mark() if hasattr(solver, "chain_mark") else None
     try:
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
                 issue_iterations(solver, n)
     except Exception as e:  # noqa: BLE001 - every failure takes the same clean-up path
+        if mark is not None:
+            solver.chain_restore(mark)
         err = "%s: %s" % (type(e).__name__, e)
         del g
         abandon_capture(s, caller)  # raises if the caller's stream is left capturing
@@ -87,6 +106,8 @@ def _capture(solver, n, tolerant):
         solver.graph_capturable = False
         warnings.warn("hipGraph capture failed; running eagerly (%s)" % err, RuntimeWarning)
         return None
+    if mark is not None:
+        solver.chain_restore(mark)  # (capturing executes nothing: the device state is unchanged)
     torch.cuda.current_stream().wait_stream(s)
     _upload(g)
     return g
@@ -169,13 +190,15 @@ def _upload(g):
 
 
 def graph_for(solver, n):
-    """The hipGraph of the exact kernel sequence of run(n) (captured once per n)."""
+    """The hipGraph of the exact kernel sequence of run(n) from the solver's current state
+    (captured once per n and, for a chaining solver, per whether a C-pass is ahead)."""
     graphs = solver.__dict__.setdefault("_graphs", {})
     if getattr(solver, "graph_capturable", True) is False:
         return None  # eager (the reason is in solver.graph_error)
-    if n not in graphs:
-        graphs[n] = _capture(solver, n, getattr(solver, "graph_tolerant", False))
-    return graphs[n]
+    key = (n, solver.ahead()) if hasattr(solver, "ahead") else n
+    if key not in graphs:
+        graphs[key] = _capture(solver, n, getattr(solver, "graph_tolerant", False))
+    return graphs[key]
 
 
 def graph_chunks(n):
@@ -191,8 +214,15 @@ def graph_chunks(n):
 def prepare_iterations(solver, n):
     """Capture (without executing) every graph that run(n, use_graph=True) will replay, so a
     later timed run(n) captures, instantiates and uploads nothing."""
-    for m in sorted(set(graph_chunks(n))):
+    if not hasattr(solver, "chain_mark"):
+        for m in sorted(set(graph_chunks(n))):
+            graph_for(solver, m)
+        return
+    mark = solver.chain_mark()
+    for m in graph_chunks(n):  # (a chaining solver's later chunks start with a C-pass ahead)
         graph_for(solver, m)
+        solver.chain_replayed()
+    solver.chain_restore(mark)
 
 
 def run_iterations(solver, n, use_graph):
@@ -207,6 +237,8 @@ def run_iterations(solver, n, use_graph):
             issue_iterations(solver, m)
         else:
             g.replay()
+            if hasattr(solver, "chain_replayed"):
+                solver.chain_replayed()
 
 
 class FreeSSolver:
@@ -222,7 +254,7 @@ class FreeSSolver:
 
     def __init__(self, obs, S_init, C_init, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
                  betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024, fuse=True,
-                 T_true=None, nmse_every=0, project_s=False):
+                 T_true=None, nmse_every=0, project_s=False, chain=True):
         self.obs = obs
         R = S_init.shape[0]
         self.R = R
@@ -239,6 +271,11 @@ class FreeSSolver:
         self.lambda_c, self.lambda_s = float(lambda_c), float(lambda_s)
         self.engine.init_state(self.S)
         self.fuse = bool(fuse) and self.engine.scpass_supported()
+        # chain: runs end with the fused launch (issue_iterations); `_ahead` says that the
+        # workspace holds the C-pass of the next iteration at the current S, C (valid while
+        # neither tensor was modified by torch since: their version counters)
+        self.chain = bool(chain)
+        self._ahead, self._ahead_ver = False, None
         self._graphs = {}
         # map NMSE after every `nmse_every`-th S-step, on the device inside the iteration
         # sequence (qsc_map_nmse_track; the reference evaluates it every iteration, :582, :637)
@@ -254,13 +291,42 @@ class FreeSSolver:
     # one outer iteration = C grad-step + S grad-step
     def c_step(self):
         e = self.engine
+        self._ahead = False
         e.cpass(self.S, self.C)
         e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)
 
     def s_step(self):
         e = self.engine
+        self._ahead = False
         e.spass(self.S, self.C, 1, mS=self.mS, vS=self.vS, adam=self.adam_s, lambda_s=self.lambda_s)
         self._track()
+
+    # ---- run chaining (issue_iterations) ----
+    def ahead(self):
+        """True when the workspace holds the next iteration's C-pass at the current S, C."""
+        return self._ahead and self._ahead_ver == (self.S._version, self.C._version)
+
+    def c_finish(self):
+        """The C-step on the C-pass a previous run left ahead (its finish only)."""
+        self._ahead = False
+        self.engine.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c,
+                            lambda_c=self.lambda_c)
+
+    def fused_last(self):
+        """The run's last S-step, fused with the next iteration's C-pass (left ahead)."""
+        e = self.engine
+        e.scpass(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s)
+        self._track()
+        self.chain_replayed()
+
+    def chain_replayed(self):
+        self._ahead, self._ahead_ver = True, (self.S._version, self.C._version)
+
+    def chain_mark(self):
+        return (self._ahead, self._ahead_ver)
+
+    def chain_restore(self, mark):
+        self._ahead, self._ahead_ver = mark
 
     def iteration(self):
         self.c_step()
@@ -269,6 +335,7 @@ class FreeSSolver:
     def fused_body(self):
         """S-step i fused with C-pass i+1, then C-step i+1's finish (needs a C-step before)."""
         e = self.engine
+        self._ahead = False
         e.scpass(self.S, self.C, self.mS, self.vS, self.adam_s, self.lambda_s)
         self._track()  # (S_{i+1}, C_{i+1}): C is updated by the cfinish below
         e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)

@@ -559,7 +559,9 @@ def test_other_rank_engine_does_not_invalidate_captured_graph():
     assert o.desc.rowfmt == 1
     ref = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32)
     ref.run(6, use_graph=False)
-    sol = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32)
+    # (chain=False: both runs replay the one graph captured here -- a chaining solver's second
+    # run would start with a C-pass ahead and replay a graph captured later)
+    sol = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, chain=False)
     sol.prepare(3)
     sol.run(3, use_graph=True)
     # an engine whose model the signed rows do not apply to (as a rank too large would)
@@ -592,6 +594,43 @@ def test_device_nmse_history_matches_host_nmse():
         sol.run(3)
         ref.append(map_nmse(sol.S_pixels(), sol.C, d["T"]))
     assert np.allclose(res.nmse, ref, rtol=1e-12, atol=0), (res.nmse, ref)
+
+
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_chained_runs_equal_one_run_and_the_unchained_form(use_graph):
+    """Runs chain through the fused launch (issue_iterations): run(a), run(b), run(c) of a
+    chaining FreeSSolver give the S, C, moments, state and history of one run(a + b + c) and of
+    the unchained form (each run closing with the stand-alone S-step) bit for bit, eager and
+    hipGraph -- also after a flush between runs (history()), and a torch-side change of S
+    between runs makes the next run redo its C-pass (no stale C-pass is finished)."""
+    from quantized_spectrum_cartography_amd.qmc import FreeSSolver
+    d = _random_case(71, 4, 96, 96, 64)
+    o = _obs(d["Y"], d["Wx"], d["b"], d["sigma"], R=4, tile=512)
+    one = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32)
+    one.run(9, use_graph=use_graph)
+    parts = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32)
+    plain = FreeSSolver(o, d["S0"], d["C0"], hist_cap=32, chain=False)
+    for n in (2, 3, 4):
+        parts.run(n, use_graph=use_graph)
+        assert parts.ahead()
+        plain.run(n, use_graph=use_graph)
+        assert not plain.ahead()
+        if n == 3:
+            parts.history()  # (a flush between runs)
+            plain.history()
+    for x in (one, plain):
+        for a, b in ((x.S, parts.S), (x.C, parts.C), (x.mS, parts.mS), (x.vS, parts.vS),
+                     (x.mC, parts.mC), (x.vC, parts.vC)):
+            assert torch.equal(a, b)
+        assert x.history() == parts.history()
+        assert x.state() == parts.state()
+    # a torch-side edit of S invalidates the C-pass left ahead
+    parts.S.mul_(1.0)
+    assert not parts.ahead()
+    plain.S.mul_(1.0)
+    parts.run(2, use_graph=use_graph)
+    plain.run(2, use_graph=use_graph)
+    assert torch.equal(parts.S, plain.S) and torch.equal(parts.C, plain.C)
 
 
 def test_phase_split_fused_launch_is_bitexact():
