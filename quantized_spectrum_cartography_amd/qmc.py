@@ -304,7 +304,8 @@ class FreeSSolver:
     # ---- run chaining (issue_iterations) ----
     def ahead(self):
         """True when the workspace holds the next iteration's C-pass at the current S, C."""
-        return self._ahead and self._ahead_ver == (self.S._version, self.C._version)
+        return (self.chain and self._ahead
+                and self._ahead_ver == (self.S._version, self.C._version))
 
     def c_finish(self):
         """The C-step on the C-pass a previous run left ahead (its finish only)."""
@@ -320,7 +321,9 @@ class FreeSSolver:
         self.chain_replayed()
 
     def chain_replayed(self):
-        self._ahead, self._ahead_ver = True, (self.S._version, self.C._version)
+        """(after a replayed or issued chaining run: its last fused launch left a C-pass ahead)"""
+        if self.chain and self.fuse:
+            self._ahead, self._ahead_ver = True, (self.S._version, self.C._version)
 
     def chain_mark(self):
         return (self._ahead, self._ahead_ver)
