@@ -1616,6 +1616,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     ac1 = acache[1];
   }
   __builtin_amdgcn_sched_barrier(0);
+  STAMP(wg, 13);  // (the C^T, edge, state reads are issued)
   int il = local_of(0);
   SliceIn<RP, E, ADAM> cur;
   const SliceLane ln = slice_lane<RP, E>(p, h);
@@ -1627,6 +1628,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   // profiles/r05/ab_early_waves.log).
   const bool early = w < QSC_EARLY_WAVES;
   auto stage = [&]() {
+    STAMP(wg, 14);  // (the wave's first-slice reads, if early, are issued)
 #if QSC_CT_VEC
     if (cvec) {
       const int Ko = sr_off(K);  // the negated half of a signed-row C^T table

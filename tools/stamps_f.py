@@ -54,6 +54,9 @@ def main():
     for nm, m in (("early", w < 4), ("late", w >= 4)):
         print("   %-5s C^T rows written" % nm, pc(st[m, 10] - st[m, 0]))
         print("   %-5s barrier passed  " % nm, pc(st[m, 1] - st[m, 10]))
+    print("  tile start -> C^T reads issued", pc(st[:, 13] - st[:, 0]))
+    print("  C^T reads issued -> staging starts", pc(st[:, 14] - st[:, 13]))
+    print("  staging starts -> C^T rows written", pc(st[:, 10] - st[:, 14]))
     print("  start->C^T (realtime, vs grid start)", pu(st[:, 28] - r0 + (st[:, 10] - st[:, 0]) / ghz * 0.1))
     if (st[:, 12] > 0).any():
         m = st[:, 12] > 0
