@@ -70,10 +70,6 @@ constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 #ifndef QSC_FAIR_PRIO
 #define QSC_FAIR_PRIO 1
 #endif
-// fused launch: the first slice's words (entry offset, width) are read ahead of the C^T reads
-#ifndef QSC_META_FIRST
-#define QSC_META_FIRST 1
-#endif
 __device__ __forceinline__ void prio_level(int lvl) {  // 3 = most urgent
   if (lvl >= 3)
     __builtin_amdgcn_s_setprio(3);
@@ -981,29 +977,6 @@ __device__ __forceinline__ SliceLane slice_lane(int p, int h) {
   return l;
 }
 
-// slice_load with the slice's words (entry offset, width) already read: the rows first (they
-// depend on nothing), then the entries
-template <int RP, typename E, bool ADAM>
-__device__ __forceinline__ void slice_load_at(SliceIn<RP, E, ADAM>& in, const E* __restrict__ ent,
-                                              int64_t o, int wd, int s, const SliceLane& ln,
-                                              const float* __restrict__ S,
-                                              const float* __restrict__ mS,
-                                              const float* __restrict__ vS) {
-  using V2 = typename Ent<E>::V2;
-  const int64_t blk = (int64_t)s * QSC_SLICE * RP;  // the slice's rows (uniform)
-  ld_row<RP>(S + blk, ln.row, in.sv);
-  if constexpr (ADAM) {
-    ld_row<RP / 2>(mS + blk, ln.half, in.mv);
-    ld_row<RP / 2>(vS + blk, ln.half, in.vv);
-  }
-  in.j1 = wd >> 2;
-  in.src = reinterpret_cast<const V2*>(ent + o);
-  const int jlast = max(in.j1 - 1, 0);
-#pragma unroll
-  for (int i = 0; i < kGroupS; ++i)
-    in.buf[i] = ld_lane(in.src + (int64_t)min(i, jlast) * (2 * QSC_SLICE), ln.ent);
-}
-
 template <int RP, typename E, bool ADAM>
 __device__ __forceinline__ void slice_load(SliceIn<RP, E, ADAM>& in, const E* __restrict__ ent,
                                            const int* __restrict__ width,
@@ -1011,12 +984,24 @@ __device__ __forceinline__ void slice_load(SliceIn<RP, E, ADAM>& in, const E* __
                                            const SliceLane& ln, const float* __restrict__ S,
                                            const float* __restrict__ mS,
                                            const float* __restrict__ vS) {
+  using V2 = typename Ent<E>::V2;
   // both slice words read before either is used: one scalar-cache round trip, not two in a
   // chain (the entry reads below depend on both; at the start of a launch this chain is the
   // critical path to the first slice's data)
   const int64_t o = off[s];
   const int wd = width[s];
-  slice_load_at(in, ent, o, wd, s, ln, S, mS, vS);
+  in.j1 = wd >> 2;
+  in.src = reinterpret_cast<const V2*>(ent + o);
+  const int jlast = max(in.j1 - 1, 0);
+#pragma unroll
+  for (int i = 0; i < kGroupS; ++i)
+    in.buf[i] = ld_lane(in.src + (int64_t)min(i, jlast) * (2 * QSC_SLICE), ln.ent);
+  const int64_t blk = (int64_t)s * QSC_SLICE * RP;  // the slice's rows (uniform)
+  ld_row<RP>(S + blk, ln.row, in.sv);
+  if constexpr (ADAM) {
+    ld_row<RP / 2>(mS + blk, ln.half, in.mv);
+    ld_row<RP / 2>(vS + blk, ln.half, in.vv);
+  }
 }
 
 // Persistent S-pass: a grid sized to the resident waves; each wave reads slice i+1 while it
@@ -1586,13 +1571,6 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   if (lane == 0 && wg < kStampWaves) g_stamps[wg * kStamps + 26] = __builtin_amdgcn_s_getreg(0xF804);
 #endif
 
-  // 0. the first slice's two words (scalar reads, QSC_META_FIRST): in flight with the C^T reads,
-  //    so the slice's entry reads need not wait for them after those are issued
-#if QSC_META_FIRST
-  const int s_first = global_of(local_of(0) < nsl ? local_of(0) : 0);
-  const int64_t o_first = s_off[s_first];
-  const int w_first = s_width[s_first];
-#endif
   // 1. C^T / edge / state reads first (the LDS staging then waits only for them: vmcnt
   //    retires in issue order), then the first slice's reads, then the staging
   const int k0 = tidx;
@@ -1723,11 +1701,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     STAMP(wg, 11);  // (wave 0: the scalars are set)
   };
   if (early) {
-#if QSC_META_FIRST
-    slice_load_at(cur, s_ent, o_first, w_first, s_first, ln, S, mS, vS);
-#else
     slice_load(cur, s_ent, s_width, s_off, global_of(il < nsl ? il : 0), ln, S, mS, vS);
-#endif
     stage();
   } else {
     stage();
