@@ -104,6 +104,11 @@ __device__ __forceinline__ void prio_level(int lvl) {  // 3 = most urgent
 #ifndef QSC_KMAP_PF
 #define QSC_KMAP_PF 1
 #endif
+// signed-row kinds (one-bit) never read the LDS edge table: the S-pass and fused launch skip
+// its read and staging, so their staging waits for the C^T reads only
+#ifndef QSC_SR_SKIP_EDGES
+#define QSC_SR_SKIP_EDGES 1
+#endif
 // fused launch: the phase split (scfused, section 3).  Off by default: its phase-A walk sits
 // between the first S-step round and the rest with the next slice's reads in flight, and at
 // 128 VGPRs (16 waves per CU) that spills (24-115 VGPRs across the instantiations); unsplit,
@@ -160,6 +165,10 @@ struct TP {
   static constexpr int v = KIND == LIK_ONEBIT_SR ? RP + 4 : Pitch<RP>::v;
 };
 constexpr bool is_sr(int kind) { return kind == LIK_ONEBIT_SR; }
+template <int KIND>
+__device__ constexpr bool stages_edges() {
+  return !(QSC_SR_SKIP_EDGES && is_sr(KIND));
+}
 // rows of a table: K (C^T) or PT (S tile), or sr_rows(rows) with signed rows (qsc_common.cuh)
 template <int KIND>
 __device__ __host__ __forceinline__ int table_rows(int rows) {
@@ -1052,7 +1061,7 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
   float c0[RP];
 #pragma unroll
   for (int r = 0; r < RP; ++r) c0[r] = C[(int64_t)min(r, R - 1) * K + min(k0, K - 1)];
-  const float2 e0 = E_.e[min(k0, nbins - 1)];
+  const float2 e0 = stages_edges<KIND>() ? E_.e[min(k0, nbins - 1)] : float2{};
   __builtin_amdgcn_sched_barrier(0);
   SliceIn<RP, E, ADAM> cur;
   const SliceLane ln = slice_lane<RP, E>(p, h);
@@ -1080,8 +1089,10 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
       put_row4<RP, KIND>(Cl, K, k, r, make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]), lk.ob_thr);
   }
   put_pad_row<RP, KIND>(Cl, K);
-  El[min(k0, nbins - 1)] = e0;  // branch-free like C^T
-  for (int b = k0 + kSBlock; b < nbins; b += kSBlock) El[b] = E_.e[b];
+  if constexpr (stages_edges<KIND>()) {
+    El[min(k0, nbins - 1)] = e0;  // branch-free like C^T
+    for (int b = k0 + kSBlock; b < nbins; b += kSBlock) El[b] = E_.e[b];
+  }
   if (threadIdx.x == 0) {
     if (ADAM) {
       const float nrm = sqrtf(st->normsq_s);
@@ -1508,6 +1519,7 @@ size_t cpass_tile_lds(int PT, int R, int nks, int NP, bool sr) {
 template <int RP>
 struct FusedBlock {
   static constexpr int v = RP > 8 ? 512 : 64 * QSC_FUSED_WAVES;
+  static constexpr int wpe = RP > 8 ? 2 : 4;  // waves per SIMD the register budget allows
 };
 
 // (device-function form: the 2 KB edge table by reference; kernel form below: by value --
@@ -1593,7 +1605,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
 #pragma unroll
   for (int r = 0; r < RP; ++r) c0[r] = C[(int64_t)min(r, R - 1) * K + min(k0, K - 1)];
 #endif
-  const float2 e0 = E_.e[min(k0, nbins - 1)];
+  const float2 e0 = stages_edges<KIND>() ? E_.e[min(k0, nbins - 1)] : float2{};
 #if QSC_KMAP_PF
   // the bins of this thread's first two part-sum outputs (step 4), read now: at the tail they
   // would be a dependent global read after the last unit
@@ -1681,8 +1693,10 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
       for (int q = k0; q < PT; q += blockDim.x) put_th<RP, KIND>(Sl, PT, q, lk.ob_thr);
       put_pad_row<RP, KIND>(Sl, PT);
     }
-    El[min(k0, nbins - 1)] = e0;
-    for (int b = k0 + (int)blockDim.x; b < nbins; b += blockDim.x) El[b] = E_.e[b];
+    if constexpr (stages_edges<KIND>()) {
+      El[min(k0, nbins - 1)] = e0;
+      for (int b = k0 + (int)blockDim.x; b < nbins; b += blockDim.x) El[b] = E_.e[b];
+    }
     STAMP(wg, 10);  // C^T rows written (its reads landed)
     if (tidx == 0) {
       const float nrm = sqrtf(nsq_s);
@@ -1947,7 +1961,8 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
 }
 
 template <int RP, typename E, int KIND, bool LOG>
-__global__ void __launch_bounds__(FusedBlock<RP>::v) scfused_kernel(QSC_SCF_KPARAMS) {
+__global__ void __launch_bounds__(FusedBlock<RP>::v, FusedBlock<RP>::wpe)
+scfused_kernel(QSC_SCF_KPARAMS) {
   scfused_tile<RP, E, KIND, LOG>(QSC_SCF_ARGS, (int)blockIdx.x, (int)gridDim.x, threadIdx.x);
 }
 
