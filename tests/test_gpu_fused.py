@@ -175,6 +175,63 @@ def test_fused_spass_cpass_bitexact(seed, R, I, J, K, log_model, loss, nbins, ti
         assert a.costs_c == b.costs_c and a.costs_s == b.costs_s
 
 
+def _edge_mask(kind, K, I, J, seed):
+    """Sampling masks at the edges of the layout: no observation at all, one observation, and
+    holes (unobserved positions, bins, and one whole 512-position tile)."""
+    g = torch.Generator().manual_seed(seed)
+    Wx = torch.zeros(K, 1, I, J)
+    if kind == "single":
+        Wx[K // 2, 0, I // 3, J - 1] = 1.0
+    elif kind == "holes":
+        Wx = torch.bernoulli(torch.full((K, 1, I, J), 0.3), generator=g)
+        flat = Wx.view(K, I * J)
+        flat[:, :64] = 0.0             # positions with no observed bin
+        flat[:, 512:1024] = 0.0        # 512 more: the count-sorted pixel order puts these 576
+        #                                together, so whole tiles are empty
+        flat[[0, 3, K - 1], :] = 0.0   # bins never observed
+    elif kind == "k1":
+        Wx = torch.bernoulli(torch.full((K, 1, I, J), 0.5), generator=g)
+    return Wx
+
+
+@pytest.mark.parametrize("kind,R,I,J,K", [("empty", 4, 40, 40, 70), ("single", 3, 33, 31, 9),
+                                          ("holes", 8, 48, 48, 130), ("k1", 2, 40, 36, 1),
+                                          ("empty", 16, 32, 32, 64)])
+def test_edge_masks_vs_oracle(kind, R, I, J, K):
+    """Empty, single-entry and holed masks, and a single frequency bin (the reference's masked sum over whatever is
+    observed, qmc/quantization_model.py:45-55, nb:571-573): the fused pass against the explicit
+    oracle, and 5 solver iterations (fused, and through a hipGraph) against the reference-form
+    solver, at the north-star 1e-5."""
+    from quantized_spectrum_cartography_amd import fused, qmc
+    d = _random_case(70 + R, R, I, J, K)
+    Wx = _edge_mask(kind, K, I, J, 70 + K)
+    obs = _obs(d["Y"], Wx, d["b"], d["sigma"], R=R)
+    assert obs.nnz == int(Wx.sum())
+    S = d["S0"].cuda().requires_grad_(True)
+    C = d["C0"].cuda().requires_grad_(True)
+    nll = fused.ProbitNLL.apply(S, C, obs)
+    nll.backward()
+    P = I * J
+    rn, rdS, rdC = explicit.nll_grad(d["S0"].reshape(R, P).numpy(), d["C0"].numpy(),
+                                     d["Y"].reshape(K, P).numpy(), Wx.reshape(K, P).numpy(),
+                                     d["b"].numpy(), d["sigma"])
+    if kind == "empty":
+        assert nll.item() == 0.0 and rn == 0.0
+        assert not S.grad.any() and not C.grad.any()
+    else:
+        assert abs(nll.item() - rn) / abs(rn) < 1e-5
+        assert rel_fro(S.grad.cpu().reshape(R, P).numpy(), rdS) < 1e-5
+        assert rel_fro(C.grad.cpu().numpy(), rdC) < 1e-5
+    ref = osolver.free_s_solve(d["S0"], d["C0"], d["Y"], Wx, d["b"], d["sigma"], n_iter=5)
+    for use_graph in (False, True):
+        res = qmc.solve(d["Y"], Wx, d["b"], d["sigma"], S_init=d["S0"], C_init=d["C0"],
+                        max_iter=5, use_graph=use_graph)
+        assert np.isfinite(res.S.cpu().numpy()).all() and np.isfinite(res.C.cpu().numpy()).all()
+        assert rel_fro(res.S.cpu().numpy(), ref["S"].numpy()) < 1e-5
+        assert rel_fro(res.C.cpu().numpy(), ref["C"].numpy()) < 1e-5
+        assert np.allclose(res.costs_c, ref["costs_c"], rtol=1e-5)
+
+
 def test_fused_solver_is_used():
     from quantized_spectrum_cartography_amd import obs as obs_mod
     from quantized_spectrum_cartography_amd.qmc import FreeSSolver
