@@ -335,6 +335,80 @@ struct Scalars {
 #ifndef QSC_DIAG_NOCONF_S
 #define QSC_DIAG_NOCONF_S 0
 #endif
+// Row addresses of signed-row entries (16-bit entries: the entry IS the row index).  The walks
+// unpack an entry straight to its row's LDS address with one v_mad_u32_u16 (op_sel picks the
+// dword's high entry): idx * pitch + the table's address, instead of a mask / shift and a
+// multiply-add per entry.  (Index form in the debug and diagnostic builds, which check or
+// rewrite the indices.)
+#ifndef QSC_SR_ADDR
+#define QSC_SR_ADDR 1
+#endif
+#if QSC_SR_ADDR && !QSC_DEBUG && !QSC_DIAG_NOLDS && !QSC_DIAG_NOCONF_C && !QSC_DIAG_NOCONF_S
+#define QSC_SR_ADDR_ON 1
+#else
+#define QSC_SR_ADDR_ON 0
+#endif
+typedef __attribute__((address_space(3))) const char lds_char;
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const f4v lds_f4v;
+typedef __attribute__((address_space(3))) const f2v lds_f2v;
+template <typename E, int KIND>
+__device__ constexpr bool sr_addr() {
+  return QSC_SR_ADDR_ON && is_sr(KIND) && sizeof(E) == 2;
+}
+__device__ __forceinline__ uint32_t mad_u16_lo(uint32_t v, uint32_t pb, uint32_t off) {
+  uint32_t r;
+  asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(r) : "v"(v), "v"(pb), "s"(off));
+  return r;
+}
+__device__ __forceinline__ uint32_t mad_u16_hi(uint32_t v, uint32_t pb, uint32_t off) {
+  uint32_t r;
+  asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(r) : "v"(v), "v"(pb), "s"(off));
+  return r;
+}
+// a gather table's LDS address (wave-uniform)
+__device__ __forceinline__ uint32_t lds_off(const float* tab) {
+  return __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(lds_char*)reinterpret_cast<const char*>(tab));
+}
+// RP floats at LDS address a as RP/2 packed pairs (lds_row2 on an LDS address)
+template <int RP>
+__device__ __forceinline__ void lds_row2_at(uint32_t a, f2v (&v)[RP / 2]) {
+#pragma unroll
+  for (int r = 0; r < RP; r += 4) {
+    const f4v x = *(lds_f4v*)(uintptr_t)(a + 4 * r);
+    v[r / 2] = f2v{x.x, x.y};
+    v[r / 2 + 1] = f2v{x.z, x.w};
+  }
+}
+// unpack 4 / 2 entries: indices, or (sr_addr) their rows' LDS byte addresses
+template <int RP, typename E, int KIND>
+__device__ __forceinline__ void ent_rows4(const typename Ent<E>::V4& v, uint32_t off,
+                                          uint32_t (&e)[4]) {
+  if constexpr (sr_addr<E, KIND>()) {
+    constexpr uint32_t PB = TP<RP, KIND>::v * 4;
+    e[0] = mad_u16_lo(v.x, PB, off);
+    e[1] = mad_u16_hi(v.x, PB, off);
+    e[2] = mad_u16_lo(v.y, PB, off);
+    e[3] = mad_u16_hi(v.y, PB, off);
+  } else {
+    (void)off;
+    Ent<E>::unpack(v, e);
+  }
+}
+template <int RP, typename E, int KIND>
+__device__ __forceinline__ void ent_rows2(const typename Ent<E>::V2& v, uint32_t off,
+                                          uint32_t (&e)[2]) {
+  if constexpr (sr_addr<E, KIND>()) {
+    constexpr uint32_t PB = TP<RP, KIND>::v * 4;
+    e[0] = mad_u16_lo(v, PB, off);
+    e[1] = mad_u16_hi(v, PB, off);
+  } else {
+    (void)off;
+    Ent<E>::unpack2(v, e);
+  }
+}
+
 // TBL: the table gathered from, 0 = C^T (S-step), 1 = the S tile (C-pass)
 template <int RP, typename E, int KIND, int TBL = 0>
 __device__ __forceinline__ void pair_rows(uint32_t ea, uint32_t eb, const f2v (&own)[RP / 2],
@@ -368,6 +442,16 @@ __device__ __forceinline__ void pair_rows(uint32_t ea, uint32_t eb, const f2v (&
   thb = splat2((float)ib);
 #else
   (void)own;
+  if constexpr (sr_addr<E, KIND>()) {
+    // ia, ib: the rows' LDS addresses (ent_rows4 / ent_rows2)
+    (void)tab;
+    (void)lk;
+    lds_row2_at<RP>(ia, oa);
+    lds_row2_at<RP>(ib, ob);
+    tha = *(lds_f2v*)(uintptr_t)(ia + RP * 4);
+    thb = *(lds_f2v*)(uintptr_t)(ib + RP * 4);
+    return;
+  }
   lds_row2<RP>(tab + ia * P, oa);
   lds_row2<RP>(tab + ib * P, ob);
   if constexpr (is_sr(KIND)) {
@@ -473,7 +557,7 @@ __device__ __forceinline__ void chunk(const typename Ent<E>::V4& v, const f2v (&
                                       const float2* __restrict__ edges, const Lik& lk,
                                       f2v (&acc)[RP / 2], f2v& nll, bool valid = true) {
   uint32_t e[4];
-  Ent<E>::unpack(v, e);
+  ent_rows4<RP, E, KIND>(v, sr_addr<E, KIND>() ? lds_off(tab) : 0u, e);
   if constexpr (is_sr(KIND)) {
     // the software-pipelined walk's arithmetic exactly (one v_log of the chunk's four P), so
     // the C-pass NLL is the same whichever walk form evaluates a chunk
@@ -539,6 +623,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
 #else
   auto fair = []() {};
 #endif
+  const uint32_t off = sr_addr<E, KIND>() ? lds_off(tab) : 0u;
   if constexpr (PFC) {
   // software-pipelined gather: the LDS rows of the next entry pair are read before the current
   // pair's arithmetic, so the LDS latency runs under it (the group's chunks are loaded, clamped,
@@ -547,7 +632,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
   f2v tra, trb;
   {
     uint32_t e[4];
-    Ent<E>::unpack(b[0], e);
+    ent_rows4<RP, E, KIND>(b[0], off, e);
     pair_rows<RP, E, KIND, 1>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
   }
   for (;;) {
@@ -560,7 +645,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
     for (int i = 0; i < kGroup; ++i)
       if (jb + i * js < j1) {
         uint32_t e[4];
-        Ent<E>::unpack(b[i], e);
+        ent_rows4<RP, E, KIND>(b[i], off, e);
         f2v xa[RP / 2], xb[RP / 2];
         f2v txa, txb, pqa, pqb;
         pair_rows<RP, E, KIND, 1>(e[2], e[3], own, tab, xa, xb, txa, txb, lk);
@@ -568,7 +653,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
                                     true);
         if (i + 1 < kGroup) {
           uint32_t f[4];
-          Ent<E>::unpack(b[i + 1], f);
+          ent_rows4<RP, E, KIND>(b[i + 1], off, f);
           pair_rows<RP, E, KIND, 1>(f[0], f[1], own, tab, ra, rb, tra, trb, lk);
         }
         pair_math<RP, E, KIND, LOG>(e[2], e[3], own, xa, xb, txa, txb, edges, lk, acc, nll, pqb,
@@ -583,7 +668,7 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
     for (int i = 0; i < kGroup; ++i) b[i] = nb[i];
     {
       uint32_t e[4];
-      Ent<E>::unpack(b[0], e);
+      ent_rows4<RP, E, KIND>(b[0], off, e);
       pair_rows<RP, E, KIND, 1>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
     }
     jb = jn;
@@ -625,6 +710,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
   j1 = __builtin_amdgcn_readfirstlane(j1);
   const int jlast = max(j1 - 1, 0);
   int jb = 0;
+  const uint32_t off = sr_addr<E, KIND>() ? lds_off(tab) : 0u;
   // (QSC_FAIR_PRIO >= 2, prio_top >= 0: the wave's level drops from prio_top to prio_top - 1
   // half-way through the slice)
   auto fair = [&]() {
@@ -637,7 +723,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
     f2v ra[RP / 2], rb[RP / 2], tra, trb;
     {
       uint32_t e[2];
-      Ent<E>::unpack2(b[0], e);
+      ent_rows2<RP, E, KIND>(b[0], off, e);
       pair_rows<RP, E, KIND, 0>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
     }
     for (;;) {
@@ -652,15 +738,15 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
       for (int i = 0; i < kGroupS; i += 2)
         if (jb + i < j1) {
           uint32_t e[2], f[2];
-          Ent<E>::unpack2(b[i], e);
-          Ent<E>::unpack2(b[i + 1], f);
+          ent_rows2<RP, E, KIND>(b[i], off, e);
+          ent_rows2<RP, E, KIND>(b[i + 1], off, f);
           f2v xa[RP / 2], xb[RP / 2], txa, txb, pa, pb = splat2(1.0f);
           pair_rows<RP, E, KIND, 0>(f[0], f[1], own, tab, xa, xb, txa, txb, lk);
           pair_math<RP, E, KIND, LOG>(e[0], e[1], own, ra, rb, tra, trb, edges, lk, acc, nll, pa,
                                       true);
           if (i + 2 < kGroupS) {
             uint32_t g[2];
-            Ent<E>::unpack2(b[i + 2], g);
+            ent_rows2<RP, E, KIND>(b[i + 2], off, g);
             pair_rows<RP, E, KIND, 0>(g[0], g[1], own, tab, ra, rb, tra, trb, lk);
           }
           if (jb + i + 1 < j1)
@@ -674,7 +760,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
       for (int i = 0; i < kGroupS; ++i) b[i] = nb[i];
       {
         uint32_t e[2];
-        Ent<E>::unpack2(b[0], e);
+        ent_rows2<RP, E, KIND>(b[0], off, e);
         pair_rows<RP, E, KIND, 0>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
       }
       jb = jn;
@@ -696,7 +782,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
           f2v pa, pb = splat2(1.0f);
           {
             uint32_t e[2];
-            Ent<E>::unpack2(b[i], e);
+            ent_rows2<RP, E, KIND>(b[i], off, e);
             f2v oa[RP / 2], ob[RP / 2], tha, thb;
             pair_rows<RP, E, KIND, 0>(e[0], e[1], own, tab, oa, ob, tha, thb, lk);
             pair_math<RP, E, KIND, LOG>(e[0], e[1], own, oa, ob, tha, thb, edges, lk, acc, nll,
@@ -704,7 +790,7 @@ __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restric
           }
           if (jb + i + 1 < j1) {
             uint32_t e[2];
-            Ent<E>::unpack2(b[i + 1], e);
+            ent_rows2<RP, E, KIND>(b[i + 1], off, e);
             f2v oa[RP / 2], ob[RP / 2], tha, thb;
             pair_rows<RP, E, KIND, 0>(e[0], e[1], own, tab, oa, ob, tha, thb, lk);
             pair_math<RP, E, KIND, LOG>(e[0], e[1], own, oa, ob, tha, thb, edges, lk, acc, nll,

@@ -87,6 +87,27 @@ def test_onebit_config_pass_and_solver(cfg, seed, fused):
     _solver_check(prob, dims, ob, expect_fused=fused)
 
 
+def test_c3_long_run_properties():
+    """C3 at full size over 120 iterations (past what the oracle can follow): size-independent
+    properties of the alternating solver (qmc/qmc.ipynb :559-634).
+      * two solvers on the same inputs agree bit for bit (graph replay of chained chunks vs one
+        eager run): the pass reductions are in a fixed order, no atomics;
+      * both costs fall: the C-step cost after the run is below the first one, and so is the
+        S-step cost;
+      * C >= 0 after every C-step projection (:579), everything finite."""
+    from quantized_spectrum_cartography_amd import qmc
+    prob, (I, J, K, R) = _onebit("c3", 20263)
+    kw = dict(S_init=prob["S0"], C_init=prob["C0"], max_iter=120)
+    a = qmc.solve(prob["Y"], prob["Wx"], prob["b"], prob["sigma"], use_graph=True, **kw)
+    b = qmc.solve(prob["Y"], prob["Wx"], prob["b"], prob["sigma"], use_graph=False, **kw)
+    assert a.fused and b.fused
+    assert np.array_equal(_np(a.S), _np(b.S)) and np.array_equal(_np(a.C), _np(b.C))
+    assert a.costs_c == b.costs_c and a.costs_s == b.costs_s
+    assert np.isfinite(_np(a.S)).all() and np.isfinite(_np(a.C)).all()
+    assert (_np(a.C) >= 0).all()
+    assert len(a.costs_c) == 120 and a.costs_c[-1] < a.costs_c[0] and a.costs_s[-1] < a.costs_s[0]
+
+
 def _c5_problem(seed=5):
     from quantized_spectrum_cartography_amd import synthetic
     prob = synthetic.c5_problem(seed=seed)
