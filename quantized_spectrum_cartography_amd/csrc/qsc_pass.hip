@@ -1605,7 +1605,7 @@ size_t cpass_tile_lds(int PT, int R, int nks, int NP, bool sr) {
 template <int RP>
 struct FusedBlock {
   static constexpr int v = RP > 8 ? 512 : 64 * QSC_FUSED_WAVES;
-  static constexpr int wpe = RP > 8 ? 2 : 4;  // waves per SIMD the register budget allows
+  static constexpr int wpe = RP > 8 ? 2 : (QSC_FUSED_WAVES + 3) / 4;  // waves per SIMD
 };
 
 // (device-function form: the 2 KB edge table by reference; kernel form below: by value --
