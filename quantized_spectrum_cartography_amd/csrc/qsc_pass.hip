@@ -1416,9 +1416,20 @@ __global__ void __launch_bounds__(kCBlock, (Occ<RP, QSC_CPASS_WAVES>::v)) cpass_
 // LDS in a fixed order (bitwise deterministic; no atomics).
 // ---------------------------------------------------------------------------------------
 constexpr int kCTBlock = 1024;
+// waves of a rank-16 tile workgroup: 8 (2 per SIMD, 256 VGPRs).  At 16 waves (128 VGPRs) the
+// rank-16 walk's 16-float C column, accumulators and pipelined gather rows spill 14-62 VGPRs
+// (tools/isa_stats.py), which made the c4k C-pass 2.3x slower per entry than rank 8
+#ifndef QSC_CTILE_W16
+#define QSC_CTILE_W16 8
+#endif
+template <int RP>
+struct CTBlock {
+  static constexpr int w = RP > 8 ? QSC_CTILE_W16 : kCTBlock / 64;  // max waves
+  static constexpr int v = 64 * w;
+};
 
 template <int RP, typename E, int KIND, bool LOG>
-__global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
+__global__ void __launch_bounds__(CTBlock<RP>::v) cpass_tile_kernel(
     const E* __restrict__ ent, const int* __restrict__ width, const int64_t* __restrict__ off,
     const int* __restrict__ kmap, int nks, int NP, int PT, Lik lk, Edges E_, int nbins, int R,
     int K,
@@ -1441,7 +1452,7 @@ __global__ void __launch_bounds__(kCTBlock) cpass_tile_kernel(
   const int Kp = nks * 64;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const float own_scale = own_scale_of<KIND, LOG>(lk);  // scaled form (lik_grad2)
-  [[maybe_unused]] const int wg = blockIdx.x * (kCTBlock / 64) + w;  // (diagnostic stamps)
+  [[maybe_unused]] const int wg = blockIdx.x * CTBlock<RP>::w + w;  // (diagnostic stamps)
   STAMP(wg, 0);
   RSTAMP(wg, 28);
 
@@ -2616,11 +2627,11 @@ int spass_bpc(int RP) { return RP > 8 ? 2 : RP == 8 ? QSC_SPASS_BPC8 : QSC_SPASS
     else if (RP == 8) LAUNCH(8, uint16_t, KD, LG);                                       \
     else LAUNCH(16, uint16_t, KD, LG);                                                   \
   } while (0)
-#ifdef QSC_DEV_ONE_VARIANT  // (ISA work: only the C3 signed-row rank-8 instantiation)
+#ifdef QSC_DEV_ONE_VARIANT  // (ISA work: only the signed-row instantiation of rank QSC_DEV_ONE_VARIANT)
 #define QSC_DISPATCH_PASS(LAUNCH)                   \
   do {                                              \
     (void)kind;                                     \
-    if (sr && RP == 8) LAUNCH(8, uint16_t, LIK_ONEBIT_SR, false); \
+    if (sr && RP == QSC_DEV_ONE_VARIANT) LAUNCH(QSC_DEV_ONE_VARIANT, uint16_t, LIK_ONEBIT_SR, false); \
     else return QSC_EUNSUPPORTED;                   \
   } while (0)
 #else
@@ -2773,7 +2784,7 @@ static int cpass_impl(const qsc_obs_desc* d, const void* c_entries, const int32_
     const int U = nks * NP;
     const size_t tshm = cpass_tile_lds(d->PT, R, nks, NP, sr);
     if (tile) {
-      const dim3 tb((unsigned)(64 * std::min(U, QSC_CTILE_MAXW)));
+      const dim3 tb((unsigned)(64 * std::min(U, RP > 8 ? QSC_CTILE_W16 : QSC_CTILE_MAXW)));
 #define CPASS_TILE_LAUNCH(RPV, ET, KD, LG)                                                     \
   hipLaunchKernelGGL((cpass_tile_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles), tb, tshm, \
                      s, (const ET*)c_entries, c_width, c_off, c_kmap, nks, NP, d->PT, lk, E,     \

@@ -38,6 +38,10 @@ class PassEngine:
         self.state = torch.zeros(_lib.STATE_BYTES, dtype=torch.uint8, device=dev)
         self.hist_cap = int(hist_cap)
         self.hist = torch.zeros(max(4 * self.hist_cap, 4), dtype=torch.float32, device=dev)
+        # workspace generation: bumped by every launch that writes the workspace's pass partials
+        # (slab, NLL / norm partials, cnsq) or C, so a solver can tell that a C-pass it left
+        # ahead in the workspace was overwritten since (qmc.FreeSSolver.ahead)
+        self.gen = 0
 
     # ---- state --------------------------------------------------------------------------
     def init_state(self, S_pos):
@@ -53,6 +57,7 @@ class PassEngine:
 
     # ---- passes -------------------------------------------------------------------------
     def cpass(self, S_pos, C):
+        self.gen += 1
         o = self.obs
         _lib.call("qsc_cpass", self.desc, _lib.ptr(self.c_entries), _lib.ptr(o.c_width), _lib.ptr(o.c_off),
                   _lib.ptr(o.c_kmap), o.model, self.R, _lib.ptr(S_pos), _lib.ptr(C),
@@ -61,6 +66,7 @@ class PassEngine:
     def cpass_nsq(self, S_pos, C):
         """cpass that also writes every slice's ||S||^2 partial (qsc_cpass_nsq: the K-slab
         C-pass after the all-gather of S, in place of a qsc_slice_nsq launch)."""
+        self.gen += 1
         o = self.obs
         _lib.call("qsc_cpass_nsq", self.desc, _lib.ptr(self.c_entries), _lib.ptr(o.c_width),
                   _lib.ptr(o.c_off), _lib.ptr(o.c_kmap), o.model, self.R, _lib.ptr(S_pos),
@@ -76,6 +82,7 @@ class PassEngine:
 
     def cfinish(self, C, mode, dC=None, mC=None, vC=None, adam=None, lambda_c=0.0,
                 normsq_ext=None, record=True):
+        self.gen += 1
         hist, cap = (self.hist, self.hist_cap) if (record and self.hist_cap) else (None, 0)
         _lib.call("qsc_cfinish", self.desc, self.R, _lib.ptr(C), int(mode), _lib.ptr(dC),
                   _lib.ptr(mC), _lib.ptr(vC), adam, float(lambda_c), _lib.ptr(normsq_ext),
@@ -83,6 +90,7 @@ class PassEngine:
                   _lib.stream())
 
     def spass(self, S_pos, C, mode, dS=None, mS=None, vS=None, adam=None, lambda_s=0.0):
+        self.gen += 1
         o = self.obs
         _lib.call("qsc_spass", self.desc, _lib.ptr(self.s_entries), _lib.ptr(o.s_width), _lib.ptr(o.s_off),
                   o.model, self.R, _lib.ptr(S_pos), _lib.ptr(C), int(mode), _lib.ptr(dS),
@@ -95,6 +103,7 @@ class PassEngine:
     def scpass(self, S_pos, C, mS, vS, adam, lambda_s):
         """spass (mode 1, Adam) fused with the next cpass at the updated S (qsc_scpass); with
         the phase split of the lists when it was computed for this rank's launch."""
+        self.gen += 1
         o = self.obs
         split = o.split_rows and o.split_rows == self.split_rows
         _lib.call("qsc_scpass", self.desc, _lib.ptr(self.s_entries), _lib.ptr(o.s_width),
@@ -106,6 +115,7 @@ class PassEngine:
                   self.ws.numel(), _lib.stream())
 
     def supdate(self, S_pos, mS, vS, g, adam, lambda_s):
+        self.gen += 1
         _lib.call("qsc_supdate", self.desc, self.R, _lib.ptr(S_pos), _lib.ptr(mS), _lib.ptr(vS),
                   _lib.ptr(g), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),
                   self.ws.numel(), _lib.stream())
@@ -116,6 +126,7 @@ class PassEngine:
     def supdate_rows(self, S_pos, mS, vS, g_own, adam, lambda_s, r0, r1):
         """Adam on position rows [r0, r1) (multiples of QSC_SLICE) from the shard's gradient
         g_own (its first row is row r0) -- qsc_supdate_slices."""
+        self.gen += 1
         u = _lib.QSC_SLICE
         if r0 % u or (r1 % u and r1 != self.obs.Pp):
             raise ValueError("shard rows must be whole position slices")
@@ -125,11 +136,13 @@ class PassEngine:
 
     def slice_nsq(self, S_pos):
         """Every slice's ||S||^2 partial from the (all-gathered) S -- qsc_slice_nsq."""
+        self.gen += 1
         _lib.call("qsc_slice_nsq", self.desc, self.R, _lib.ptr(S_pos), _lib.ptr(self.ws),
                   self.ws.numel(), _lib.stream())
 
     def cupdate(self, C, mC, vC, g, adam, lambda_c, normsq_s_ext=None):
         """C update from an all-reduced gradient g (R*K [+1]) (IJ-slab sharding)."""
+        self.gen += 1
         _lib.call("qsc_cupdate", self.R, self.obs.K, _lib.ptr(C), _lib.ptr(mC), _lib.ptr(vC),
                   _lib.ptr(g), adam, float(lambda_c), _lib.ptr(normsq_s_ext),
                   _lib.ptr(self.state), _lib.stream())

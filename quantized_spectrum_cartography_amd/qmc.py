@@ -218,10 +218,15 @@ def prepare_iterations(solver, n):
         for m in sorted(set(graph_chunks(n))):
             graph_for(solver, m)
         return
+    # A chaining solver's graphs are keyed by whether a C-pass is ahead: run(n) from the current
+    # state replays (m, ahead()) for its first chunk and (m, True) for the later ones, and a later
+    # run(n) starts with a C-pass ahead.  Capture both entry forms of every chunk size, so no
+    # later run(n) captures anything whatever state it starts from.
     mark = solver.chain_mark()
-    for m in graph_chunks(n):  # (a chaining solver's later chunks start with a C-pass ahead)
-        graph_for(solver, m)
-        solver.chain_replayed()
+    for m in sorted(set(graph_chunks(n))):
+        for a in (False, True):
+            if solver.chain_force(a):
+                graph_for(solver, m)
     solver.chain_restore(mark)
 
 
@@ -254,7 +259,7 @@ class FreeSSolver:
 
     def __init__(self, obs, S_init, C_init, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
                  betas=(0.9, 0.999), eps=1e-8, project_c=True, hist_cap=1024, fuse=True,
-                 T_true=None, nmse_every=0, project_s=False, chain=True):
+                 T_true=None, nmse_every=0, project_s=None, chain=True):
         self.obs = obs
         R = S_init.shape[0]
         self.R = R
@@ -266,8 +271,13 @@ class FreeSSolver:
         self.adam_c = _lib.make_adam(lr_c, betas, eps, project_nonneg=project_c)
         # project_s: S >= 0 after every S-step (S[S<0] = 0, fused into the S-side Adam), the
         # domain of the reference's generator / decoder S (sigmoid outputs, deep_prior/networks/
-        # dip.py:80); for free S under the log model, where T_hat + offset must stay > 0
-        self.adam_s = _lib.make_adam(lr_s, betas, eps, project_nonneg=project_s)
+        # dip.py:80).  Default (None): on under the log model, where T_hat + offset must stay > 0
+        # -- unprojected free S drives T_hat + offset <= 0 within ~200 iterations at C5
+        # (log of a non-positive value: a non-finite cost and S); off otherwise
+        if project_s is None:
+            project_s = bool(getattr(obs, "log_model", False))
+        self.project_s = bool(project_s)
+        self.adam_s = _lib.make_adam(lr_s, betas, eps, project_nonneg=self.project_s)
         self.lambda_c, self.lambda_s = float(lambda_c), float(lambda_s)
         self.engine.init_state(self.S)
         self.fuse = bool(fuse) and self.engine.scpass_supported()
@@ -302,10 +312,17 @@ class FreeSSolver:
         self._track()
 
     # ---- run chaining (issue_iterations) ----
+    def _chain_key(self):
+        """What a C-pass left ahead depends on: S and C (their storage and torch version
+        counters: an in-place torch write, or a fresh tensor swapped in) and the workspace it
+        sits in (the engine's launch generation: any pass or finish launched on the engine since,
+        by this solver or by a caller such as bench.time_kernel, may have overwritten it)."""
+        return (self.S.data_ptr(), self.S._version, self.C.data_ptr(), self.C._version,
+                self.engine.gen)
+
     def ahead(self):
         """True when the workspace holds the next iteration's C-pass at the current S, C."""
-        return (self.chain and self._ahead
-                and self._ahead_ver == (self.S._version, self.C._version))
+        return self.chain and self._ahead and self._ahead_ver == self._chain_key()
 
     def c_finish(self):
         """The C-step on the C-pass a previous run left ahead (its finish only)."""
@@ -323,13 +340,23 @@ class FreeSSolver:
     def chain_replayed(self):
         """(after a replayed or issued chaining run: its last fused launch left a C-pass ahead)"""
         if self.chain and self.fuse:
-            self._ahead, self._ahead_ver = True, (self.S._version, self.C._version)
+            self._ahead, self._ahead_ver = True, self._chain_key()
 
     def chain_mark(self):
-        return (self._ahead, self._ahead_ver)
+        return (self._ahead, self._ahead_ver, self.engine.gen)
 
     def chain_restore(self, mark):
-        self._ahead, self._ahead_ver = mark
+        # (a capture issues launches without executing them: the engine's generation returns to
+        # its value before the capture, so the captured run does not invalidate the state)
+        self._ahead, self._ahead_ver, self.engine.gen = mark
+
+    def chain_force(self, ahead):
+        """Set the chaining state run() starts from (prepare: capture both entry forms)."""
+        if ahead:
+            self.chain_replayed()
+        else:
+            self._ahead = False
+        return self.ahead() == bool(ahead)
 
     def iteration(self):
         self.c_step()
@@ -401,7 +428,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
           betas=(0.9, 0.999), eps=1e-8, project_c=True, generator=None, Z_init=None,
           restart=False, restart_samples=(200, 200), T_true=None, nmse_every=0,
           use_graph=False, obs=None, tile=None, callback=None, loss="probit", fuse=True,
-          project_s=False):
+          project_s=None):
     """Alternating S/C probit-MLE (qmc/qmc.ipynb :559-645).
 
     Args mirror the notebook globals: Y (K,1,I,J) bin indices, Wx (K,1,I,J) 0/1 mask,
@@ -411,8 +438,11 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
     loss="squared" replaces the probit likelihood by the Euclidean criterion
     ||Wx (T_hat - Obs)||_F^2 of qmc/qmc_dowjons.ipynb :142-162 (Obs = bin midpoints,
     get_quantized_obs_from_ordinal); the cost history then holds that criterion.
-    project_s=True keeps free S >= 0 (S[S<0] = 0 after each S-step, as C at :579): the log
-    model needs T_hat + offset > 0, which free S can otherwise leave.
+    project_s=True keeps free S >= 0 (S[S<0] = 0 after each S-step, as C at :579).  The
+    default (None) is True for the log model: it needs T_hat + offset > 0 (log at
+    qmc/quantization_model_log.py:14, qmc/qmc.ipynb:571), which unprojected free S leaves within
+    a few hundred steps, and the reference's own S is a sigmoid output (>= 0); False otherwise.
+    project_s=False under the log model is accepted (the caller's choice) and warns.
     Returns a SolveResult with S (R,1,I,J) and C (R,K) on the GPU.
     """
     if log_model and obs is None:
@@ -433,6 +463,11 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
     if generator is None:
         if S_init is None:
             S_init = torch.zeros(R, 1, I, J)
+        if project_s is None:
+            project_s = bool(obs.log_model)
+        elif log_model and not project_s:
+            warnings.warn("free S under the log model without project_s: T_hat + offset can "
+                          "reach <= 0 (a non-finite cost)", RuntimeWarning)
         # the NMSE history is recorded on the device inside the run (no host round trips);
         # a callback still gets control every nmse_every iterations (or once at the end)
         sol = FreeSSolver(obs, S_init, C_init, lambda_c, lambda_s, lr_c, lr_s, betas, eps,

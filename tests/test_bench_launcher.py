@@ -110,8 +110,47 @@ def test_extra_measurement_plan(monkeypatch):
         return {}, _Obs(), object()
 
     monkeypatch.setattr(bench, "build_solver", fake_build)
-    monkeypatch.setattr(bench, "timed_run", lambda *a, **k: (2.0, 2.0))
+    monkeypatch.setattr(bench, "timed_run", lambda *a, **k: (2.0, 2.0, 1e-4))
     a = _args(["--gpus", "4", "--steps", "10"])
     out = bench.extra_measurements((8, 8, 8, 2), a, 1, 4, None, "strong", "kslab")
     assert built == [("strong", "ijslab"), ("weak", "ijslab")]
     assert out["layouts"]["ijslab"]["value"] == 5.0 and out["weak"]["ijslab"]["value"] == 20.0
+
+
+def _kslab_breakdown():
+    k = {"cpass_nsq": {"us": 15.0, "bytes": 30e6, "symbol": "cpass_tile_kernel", "what": "C"},
+         "cfinish": {"us": 4.0, "bytes": 1e6, "symbol": "cfinish_kernel", "what": "F"},
+         "spass_grad": {"us": 12.0, "bytes": 40e6, "symbol": "spass_kernel", "what": "S"},
+         "supdate_rows": {"us": 2.0, "bytes": 3e6, "symbol": "supdate", "what": "A"}}
+    return {"kernels": k, "collectives": {"allreduce_cnsq": {"us": 9.0}}}
+
+
+def test_kslab_roofline_names_a_kernel_the_layout_runs():
+    """under K-slab the line's roofline is the dominant kernel of the K-slab
+    iteration (spass mode 0 / cpass_nsq / ...) with its own bytes, never the fused S-step."""
+    r = bench.select_roofline(True, _kslab_breakdown(), 1e-5, 1.0, 2e-5, 2.0, 0)
+    assert r["symbol"] == "cpass_tile_kernel" and r["bytes"] == 30e6 and abs(r["t"] - 15e-6) < 1e-12
+    assert "scfused" not in r["kernel"] and "spass_kernel (fused" not in r["kernel"]
+
+
+def test_fused_roofline_uses_the_longer_of_self_replay_and_in_sequence():
+    """frac uses the lower of the two fractions."""
+    r = bench.select_roofline(True, None, 1e-5, 1.0, 27.4e-6, 77.2e6, 2.2e6,
+                              {"scfused_us": 29.3})
+    assert r["symbol"] == "scfused_kernel" and abs(r["t"] - 29.3e-6) < 1e-12
+    assert r["t_self_replay"] == 27.4e-6 and abs(r["t_in_sequence"] - 29.3e-6) < 1e-12
+    r = bench.select_roofline(True, None, 1e-5, 1.0, 27.4e-6, 77.2e6, 2.2e6, {"error": "x"})
+    assert r["t"] == 27.4e-6 and r["t_in_sequence"] is None
+    r = bench.select_roofline(False, None, 1e-5, 1.0, None, None, 0)
+    assert r["symbol"] == "spass_kernel"
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_kslab_projection_keys(world):
+    """Every strong K-slab C3 line carries DESIGN section 5's projection; other runs none."""
+    p = bench.projection("c3", world, "kslab", "strong")
+    lo, hi = p["iteration_us"]
+    assert 0 < lo <= hi and p["grad_steps_per_s"] == [2e6 / hi, 2e6 / lo]
+    assert bench.projection("c3", world, "ijslab", "strong") is None
+    assert bench.projection("c3", world, "kslab", "weak") is None
+    assert bench.projection("c3", 1, "kslab", "strong") is None

@@ -68,7 +68,8 @@ def _solver_check(prob, dims, ob, iters=3, log_model=False, offset=0.0, expect_f
     P = I * J
     res = qmc.solve(prob["Y"], prob["Wx"], prob["b"], prob["sigma"], S_init=prob["S0"],
                     C_init=prob["C0"], max_iter=iters, log_model=log_model,
-                    offset=offset if log_model else None, use_graph=True, lr_c=lr_c, lr_s=lr_s)
+                    offset=offset if log_model else None, use_graph=True, lr_c=lr_c, lr_s=lr_s,
+                    project_s=False)  # (the oracle's explicit solve does not project S)
     if expect_fused is not None:
         assert res.fused == expect_fused
     S, C, cc, cs = explicit.explicit_solve(_np(prob["S0"], (R, P)), _np(prob["C0"]), ob,
@@ -123,6 +124,22 @@ def test_c5_log_model_pass_and_solver():
     # S = G(Z) is a sigmoid output and cannot go negative), so lr_s is scaled to S
     _solver_check(prob, dims, ob, log_model=True, offset=off, lr_s=1e-5)
     assert np.isfinite(ob[0]).all()
+
+
+def test_c5_free_s_log_model_default_stays_finite():
+    """free S under the log model with the DEFAULT arguments (lr_s 1e-2, the
+    solver's own default S >= 0 projection) stays finite over 200 iterations at C5 -- without the
+    projection T_hat + offset reached <= 0 within 200 steps and the cost went non-finite
+    (gpurun_out/r05b/bench_c5.log)."""
+    from quantized_spectrum_cartography_amd import qmc
+    prob, dims, off = _c5_problem()
+    res = qmc.solve(prob["Y"], prob["Wx"], prob["b"], prob["sigma"], S_init=prob["S0"],
+                    C_init=prob["C0"], max_iter=200, log_model=True, offset=off, use_graph=True)
+    S, C = _np(res.S), _np(res.C)
+    assert np.isfinite(S).all() and np.isfinite(C).all()
+    assert (S >= 0).all() and (C >= 0).all()
+    assert np.isfinite(res.costs_c).all() and np.isfinite(res.costs_s).all()
+    assert res.costs_s[-1] < res.costs_s[0]
 
 
 def test_c5_dip_fused_dS_isolated():

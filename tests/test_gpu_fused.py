@@ -114,9 +114,11 @@ def test_solver_vs_reference_golden(golden, name):
     n = int(g["n_iter"])
     Y = T(g["Y"].astype(np.int64))
     Wx = T(g["Wx"].astype(np.float32))
+    # (project_s=False: the reference's free-S solver never projects S, so neither did the run
+    # that made the goldens; the log model's default projection is the build's safeguard)
     kw = dict(offset=float(g["offset"]), log_model=bool(g["log_model"]),
               lambda_c=float(g["lam_c"]), lambda_s=float(g["lam_s"]), lr_c=float(g["lr_c"]),
-              lr_s=float(g["lr_s"]))
+              lr_s=float(g["lr_s"]), project_s=False)
     r1 = qmc.solve(Y, Wx, T(g["b"]), float(g["sigma"]), S_init=T(g["S0"]), C_init=T(g["C0"]),
                    max_iter=1, **kw)
     assert rel_fro(r1.S.cpu().numpy(), g["S_it1"]) < 1e-5
@@ -482,7 +484,7 @@ def test_squared_solver_vs_reference_golden(golden):
     n = int(g["n_iter"])
     kw = dict(offset=float(g["offset"]), log_model=True, lambda_c=float(g["lam_c"]),
               lambda_s=float(g["lam_s"]), lr_c=float(g["lr_c"]), lr_s=float(g["lr_s"]),
-              loss="squared")
+              loss="squared", project_s=False)
     args = (T(g["Y"].astype(np.int64)), T(g["Wx"].astype(np.float32)), T(g["b"]),
             float(g["sigma"]))
     r1 = qmc.solve(*args, S_init=T(g["S0"]), C_init=T(g["C0"]), max_iter=1, **kw)
