@@ -333,6 +333,18 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
                       const float* C, int32_t mode, float* dS, float* mS, float* vS,
                       const qsc_adam* adam, float lambda_s, qsc_state* st, void* ws,
                       size_t ws_bytes, void* stream);
+/* K-slab S-pass (north-star sharding; the gradient half of the S-step, qmc/qmc.ipynb :626-633,
+ * over this rank's bins): qsc_spass mode 0 with dS written in the reduce-scatter layout of
+ * nranks chunks of chunk_slices position slices, each followed by ONE extra slice
+ * (dS_rs[nranks][chunk_slices + 1][QSC_SLICE][RP]), and ||C_slab||^2 of the C it read stored in
+ * element 0 of every chunk's extra slice -- so the reduce-scatter of dS_rs hands every rank the
+ * summed gradient of its rows AND the global ||C||^2 the next C-step's non-squared regulariser
+ * needs (no separate all-reduce).  Other extra-slice elements are left untouched (keep them 0).
+ * Needs chunk_slices * nranks >= Pp / QSC_SLICE. */
+QSC_API int qsc_spass_kslab(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
+                            const int64_t* s_off, const qsc_model* m, int32_t R, float* S,
+                            const float* C, float* dS_rs, int32_t chunk_slices, int32_t nranks,
+                            qsc_state* st, void* ws, size_t ws_bytes, void* stream);
 /* C-pass: per-tile partial dC slab + NLL partials into ws. */
 QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_t* c_width,
                       const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m, int32_t R,

@@ -1109,7 +1109,7 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
     const float* __restrict__ C, float* __restrict__ dS, float* __restrict__ mS,
     float* __restrict__ vS, qsc_adam ad, float lambda_s, qsc_state* __restrict__ st,
     float* __restrict__ part_nll, float* __restrict__ part_nsq, int* __restrict__ sched,
-    AdamCache* __restrict__ acache) {
+    AdamCache* __restrict__ acache, int ck, int nck) {
   constexpr int CP = TP<RP, KIND>::v;
   constexpr int RH = RP / 2;  // row elements updated per lane (half row)
   // linear models evaluate the entries in a scaled form (lik_grad2)
@@ -1256,7 +1256,9 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
       nsq = wave_sum_dpp(nsq);
       if (lane == 0) part_nsq[s] = nsq;
     } else {
-      st_row_wt<RH>(dS + blk, ln.half, a);
+      // (K-slab, ck > 0: the reduce-scatter layout, one extra slice after every ck slices)
+      const int64_t dblk = ck > 0 ? (int64_t)(s + s / ck) * QSC_SLICE * RP : blk;
+      st_row_wt<RH>(dS + dblk, ln.half, a);
     }
     const float nll_w = wave_sum_dpp(nll.x + nll.y) * kLn2;
     if (lane == 0) part_nll[s] = nll_w;
@@ -1274,6 +1276,25 @@ __global__ void __launch_bounds__(kSBlock, (OccS<RP, (int)sizeof(E), QSC_SPASS_W
   }
   // the next S-step's scalars (cfinish settles step_s + 1 in between)
   if (ADAM && blockIdx.x == 0 && threadIdx.x == 0) adam_cache_store(acache, ad, st->step_s + 2);
+  if constexpr (!ADAM) {
+    // K-slab (ck > 0): ||C_slab||^2 of the C this pass read -- the C the next C-step
+    // differentiates -- into the extra slice of every rank's chunk of the reduce-scatter buffer,
+    // so the reduce-scatter of dS delivers every rank the GLOBAL ||C||^2 with its gradient rows
+    // (no all-reduce of its own).  Order of cnorm_sq (thread t < 256 accumulates t, t + 256, ...
+    // then the block sum): the same bits as the C-pass's ||C||^2.  (Sc's scratch is free here.)
+    if (ck > 0 && blockIdx.x == 0) {
+      float s2 = 0.0f;
+      if (threadIdx.x < 256)
+        for (int i2 = threadIdx.x; i2 < R * K; i2 += 256) {
+          const int r = i2 / K, k = i2 - r * K;
+          const float c = Cl[k * CP + r];
+          s2 = __builtin_fmaf(c, c, s2);
+        }
+      const float nsq = block_sum(s2, smem);
+      if (threadIdx.x == 0)
+        for (int c = 0; c < nck; ++c) dS[(int64_t)(c * (ck + 1) + ck) * QSC_SLICE * RP] = nsq;
+    }
+  }
   STAMP(w, kStampLast);
   RSTAMP(w, 29);
 }
@@ -2075,9 +2096,16 @@ size_t scfused_lds(int PT, int R, int K, int nks, int NP, bool sr) {
 // for both row formats), the tile form's LDS fits and so does the fused launch's where it can
 // fit at all; true when the tile form applies (>= 4 units, LDS fits at the layout's own row
 // format `sr`)
+// rank 16: units (k-slices x parts) per tile at most -- 8, one per wave of the 8-wave
+// workgroups: c4k K-slab C-pass 24.8 us at 16 units (two per wave), 22.6 us at 8, 22.7 us with
+// 12 units on 12-wave workgroups (profiles/r06/r16/ab_r16_units_waves.log)
+#ifndef QSC_R16_UNITS
+#define QSC_R16_UNITS 8
+#endif
 static bool tile_parts(const qsc_obs_desc* d, int R, bool sr, int* np) {
   const int nks = d->nks;
-  int NP = nks >= QSC_CTILE_MAXW ? 1 : QSC_CTILE_MAXW / nks;
+  const int maxu = R > 8 ? QSC_R16_UNITS : QSC_CTILE_MAXW;
+  int NP = nks >= maxu ? 1 : maxu / nks;
   const double chunks = (double)d->nnz / ((double)d->ntiles * d->K) / 4.0;
   const bool fused = scfused_lds(d->PT, R, d->K, nks, 1, true) <= 160 * 1024;
   while (NP > 1 && (chunks / NP < QSC_CPART_MIN_CHUNKS ||
@@ -2673,11 +2701,38 @@ QSC_API int qsc_state_init(qsc_state* st, const float* S, int32_t R, int32_t Pp,
   return QSC_OK;
 }
 
+static int spass_impl(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
+                      const int64_t* s_off, const qsc_model* m, int32_t R, float* S,
+                      const float* C, int32_t mode, float* dS, float* mS, float* vS,
+                      const qsc_adam* adam, float lambda_s, qsc_state* st, void* ws,
+                      size_t ws_bytes, void* stream, int ck, int nck);
+
 QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
                       const int64_t* s_off, const qsc_model* m, int32_t R, float* S,
                       const float* C, int32_t mode, float* dS, float* mS, float* vS,
                       const qsc_adam* adam, float lambda_s, qsc_state* st, void* ws,
                       size_t ws_bytes, void* stream) {
+  return spass_impl(d, s_entries, s_width, s_off, m, R, S, C, mode, dS, mS, vS, adam, lambda_s,
+                    st, ws, ws_bytes, stream, 0, 0);
+}
+
+QSC_API int qsc_spass_kslab(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
+                            const int64_t* s_off, const qsc_model* m, int32_t R, float* S,
+                            const float* C, float* dS_rs, int32_t chunk_slices, int32_t nranks,
+                            qsc_state* st, void* ws, size_t ws_bytes, void* stream) {
+  const int nslices = d ? d->Pp / QSC_SLICE : 0;
+  if (!d || chunk_slices < 1 || nranks < 1 || (int64_t)chunk_slices * nranks < nslices ||
+      !dS_rs)
+    return QSC_EINVAL;
+  return spass_impl(d, s_entries, s_width, s_off, m, R, S, C, 0, dS_rs, nullptr, nullptr,
+                    nullptr, 0.0f, st, ws, ws_bytes, stream, chunk_slices, nranks);
+}
+
+static int spass_impl(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
+                      const int64_t* s_off, const qsc_model* m, int32_t R, float* S,
+                      const float* C, int32_t mode, float* dS, float* mS, float* vS,
+                      const qsc_adam* adam, float lambda_s, qsc_state* st, void* ws,
+                      size_t ws_bytes, void* stream, int ck, int nck) {
   if (!desc_ok(d) || !m || m->nbounds - 1 != d->nbins || R < 1 || R > QSC_MAX_R || !S || !C ||
       !s_width || !s_off || (d->s_entries > 0 && !s_entries) || !ws || !st ||
       ws_bytes < ws_bytes_for(d, R))
@@ -2712,12 +2767,12 @@ QSC_API int qsc_spass(const qsc_obs_desc* d, const void* s_entries, const int32_
       hipLaunchKernelGGL((spass_kernel<RPV, ET, KD, LG, true>), grid, dim3(kSBlock), shm, s,   \
                          (const ET*)s_entries, s_width, s_off, nslices, lk, E, d->nbins, R,    \
                          d->K, d->Pp, S, C, dS, mS, vS, ad, lambda_s, st, w.snll, w.snsq,       \
-                         w.sched, w.acache);                                                   \
+                         w.sched, w.acache, 0, 0);                                             \
     else                                                                                       \
       hipLaunchKernelGGL((spass_kernel<RPV, ET, KD, LG, false>), grid, dim3(kSBlock), shm, s,  \
                          (const ET*)s_entries, s_width, s_off, nslices, lk, E, d->nbins, R,    \
                          d->K, d->Pp, S, C, dS, mS, vS, ad, lambda_s, st, w.snll, w.snsq,       \
-                         w.sched, w.acache);                                                   \
+                         w.sched, w.acache, ck, nck);                                          \
   } while (0)
   QSC_DISPATCH_PASS(SPASS_LAUNCH);
 #undef SPASS_LAUNCH

@@ -13,7 +13,7 @@ import torch
 
 from .nets import DecoderDip, SizedDecoderDip
 from .obs import Observations
-from .qmc import _solve_generator
+from .qmc import GeneratorSolver, drive_generator
 from .utils import LOG_OFFSET_7_ADJUSTED as LOG_OFFSET
 
 
@@ -74,7 +74,8 @@ def solve(Y, Wx, bin_boundaries, noise_std, R, offset=None, log_model=True, deco
           Z_init=None, C_init=None, lambda_c=100.0, lambda_s=100.0, lr_c=5e-3, lr_s=1e-2,
           max_iter=500, optimize="weights", T_true=None, nmse_every=0, obs=None, tile=None,
           seed=0, callback=None, S_init=None, prefit_steps=1000, prefit_lr=1e-2, ndf=16,
-          warm="residual", residual_scale=None, lr_c_rel=1e-2, calibrate=True):
+          warm="residual", residual_scale=None, lr_c_rel=1e-2, calibrate=True, use_graph=True,
+          build_only=False, hist_cap=None):
     """DIP-regularised alternating probit MLE (config 5: log model + DIP prior on S).
 
     `offset` defaults to the reference log model's LOG_OFFSET_7_ADJUSTED
@@ -104,7 +105,13 @@ def solve(Y, Wx, bin_boundaries, noise_std, R, offset=None, log_model=True, deco
     S_start the S the solve starts from -- so from the notebook's zero C the C-step reaches the
     data's scale in ~1/lr_c_rel steps instead of overshooting it by orders of magnitude (a
     generated C5 map has T ~ 1e-5: at 5e-3 the cold start oscillates to map NMSE ~4, profiles/r04/
-    quality.json).  The value used is returned as result.lr_c."""
+    quality.json).  The value used is returned as result.lr_c.
+
+    use_graph=True (default): after one eager iteration the iterations run as captured hipGraph
+    chunks (qmc.GeneratorSolver: decoder forward / backward, its optimizer step and the fused HIP
+    passes, no host synchronisation per iteration); result.graph_error says why not if a capture
+    failed.  build_only=True returns the qmc.GeneratorSolver without running it (bench.py's
+    --config c5dip times its run(); hist_cap bounds its cost history, default max_iter)."""
     if log_model:
         offset = LOG_OFFSET if offset is None else float(offset)
         if not offset > 0.0:
@@ -158,9 +165,14 @@ def solve(Y, Wx, bin_boundaries, noise_std, R, offset=None, log_model=True, deco
             s_mean = float(net(Zp).abs().mean())
         lr_c = float(lr_c_rel) * _c_target(Y, Wx, bin_boundaries, noise_std, R, s_mean,
                                             offset if log_model else 0.0, log_model)
-    res = _solve_generator(obs, net, Zp, C_init, R, lambda_c, lambda_s, lr_c, lr_s, max_iter,
-                           (0.9, 0.999), 1e-8, True, False, (0, 0), T_true, nmse_every, callback,
-                           params=params, optimize_z=optimize in ("z", "both"))
+    sol = GeneratorSolver(obs, net, Zp, C_init, R, lambda_c, lambda_s, lr_c, lr_s,
+                          (0.9, 0.999), 1e-8, True, params=params,
+                          optimize_z=optimize in ("z", "both"), hist_cap=hist_cap or max_iter)
+    sol.decoder = decoder
+    sol.lr_c = float(lr_c)
+    if build_only:
+        return sol
+    res = drive_generator(sol, max_iter, False, (0, 0), T_true, nmse_every, callback, use_graph)
     res.decoder = decoder
     res.lr_c = float(lr_c)
     return res

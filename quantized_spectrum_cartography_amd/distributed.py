@@ -17,17 +17,22 @@ outer iteration
           rebuilds every slice's ||S||^2 partial from the S tile it stages); the non-squared
           regulariser lambda_c ||C||_F needs the GLOBAL ||C||^2, so the ranks all-reduce that
           one float in place before the fused cfinish (Adam + projection);
-  S-step: local S-pass in gradient mode (partial dS over the slab's bins); a REDUCE-SCATTER of
-          dS (Pp x RP fp32, 8.4 MB at 512x512, R = 8) leaves rank g the summed gradient of its
-          1/N of the position slices; Adam on those rows only (qsc_supdate_slices: 1/N of the
-          S/mS/vS traffic); an ALL-GATHER of the updated shards (in place in S) re-replicates S;
-          the next C-pass rebuilds the per-slice ||S_new||^2 partials from the gathered S
-          (bit-identical to the ones the shard updates produced), so the regulariser norm of
-          the next step is the same on all ranks without another collective (before a final
-          flush, history() runs qsc_slice_nsq for the last iteration).
+  S-step: local S-pass in gradient mode (qsc_spass_kslab: partial dS over the slab's bins,
+          written in the reduce-scatter layout -- N chunks of whole position slices, each
+          followed by one extra slice that carries this slab's ||C_new||^2, the norm of the C
+          the pass read); a REDUCE-SCATTER of that buffer (Pp x RP fp32, 8.4 MB at 512x512,
+          R = 8) leaves rank g the summed gradient of its 1/N of the position slices AND the
+          global ||C||^2 the next C-step's regulariser needs; Adam on the owned rows only
+          (qsc_supdate_slices: 1/N of the S/mS/vS traffic); an ALL-GATHER of the updated shards
+          (in place in S) re-replicates S; the next C-pass rebuilds the per-slice ||S_new||^2
+          partials from the gathered S (bit-identical to the ones the shard updates produced),
+          so the regulariser norm of the next step is the same on all ranks without another
+          collective (before a final flush, history() runs qsc_slice_nsq for the last iteration).
           Same bytes on the fabric as one all-reduce, 1/N of the Adam traffic per rank.
-An iteration is 4 kernels (cpass_nsq, cfinish, spass, supdate_slices) and 3 collectives
-(all-reduce of 1 float, reduce-scatter and all-gather of S-sized buffers).
+An iteration is 4 kernels (cpass_nsq, cfinish, spass_kslab, supdate_slices) and 2 collectives
+(reduce-scatter and all-gather of S-sized buffers).  The ||C||^2 rides on the reduce-scatter:
+only the first C-step of a run, whose C no S-pass has normed yet (C may have been changed by
+the caller between runs), all-reduces the C-pass's ||C_slab||^2 itself.
 The next C-pass reads every tile's new S rows, which exist only after the all-gather, so the
 S update cannot be fused into it the way qsc_scpass fuses IJ-slab's.
 The pixel order of S (positions) is derived from the GLOBAL per-pixel observation counts
@@ -197,10 +202,17 @@ class KSlabSolver:
         self.S_buf = torch.zeros((rows,) + tuple(S_pos.shape[1:]), dtype=torch.float32, device=dev)
         self.S_buf[:Pp] = S_pos
         self.S = self.S_buf[:Pp]
-        self.dS_buf = torch.zeros_like(self.S_buf)
-        self.dS = self.dS_buf[:Pp]
-        self.dS_own = torch.zeros((self.chunk,) + tuple(S_pos.shape[1:]), dtype=torch.float32,
-                                  device=dev)
+        # the reduce-scatter buffer: ws chunks of `chunk` gradient rows, each followed by one
+        # extra slice (`unit` rows) whose first element carries this slab's ||C||^2
+        # (qsc_spass_kslab); the rest of the extra slices stays zero
+        self.unit = unit
+        self.nranks = ws
+        self.dS_buf = torch.zeros((ws * (self.chunk + unit),) + tuple(S_pos.shape[1:]),
+                                  dtype=torch.float32, device=dev)
+        self.dS_own = torch.zeros((self.chunk + unit,) + tuple(S_pos.shape[1:]),
+                                  dtype=torch.float32, device=dev)
+        # the global ||C||^2 the reduce-scatter delivers (1-float view of this rank's extra slice)
+        self.nsq_rs = self.dS_own[self.chunk].reshape(-1)[:1]
         self.C = C_init_local.detach().to(dev, torch.float32).reshape(R, obs.K).clone()
         self.mS, self.vS = torch.zeros_like(self.S), torch.zeros_like(self.S)
         self.mC, self.vC = torch.zeros_like(self.C), torch.zeros_like(self.C)
@@ -217,16 +229,26 @@ class KSlabSolver:
         if not self.graph_capturable:
             self.graph_error = "collectives over %s are not graph-capturable" % dist.get_backend()
 
+    def begin_run(self):
+        """(issue_iterations, at the start of every run): the run's first C-step all-reduces
+        the C-pass's ||C_slab||^2, later ones take the one the reduce-scatter delivered."""
+        self._rs_norm = False
+
     def c_step(self):
         e = self.engine
         e.cpass_nsq(self.S, self.C)  # + ||C_slab||^2 into nsq_c, + the slices' ||S||^2
-        self.dist.all_reduce(self.nsq_c)
+        if getattr(self, "_rs_norm", False):
+            nsq = self.nsq_rs  # global ||C||^2 from the previous S-step's reduce-scatter
+        else:
+            self.dist.all_reduce(self.nsq_c)
+            nsq = self.nsq_c
         e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c,
-                  normsq_ext=self.nsq_c)
+                  normsq_ext=nsq)
 
     def s_step(self):
         e = self.engine
-        e.spass(self.S, self.C, 0, dS=self.dS)
+        # partial dS (+ ||C_slab||^2 of the updated C) in the reduce-scatter layout
+        e.spass_kslab(self.S, self.C, self.dS_buf, self.chunk, self.nranks)
         # reduce-scatter -> Adam on the owned rows -> all-gather (in place in S_buf)
         self.dist.reduce_scatter_tensor(self.dS_own, self.dS_buf)
         e.supdate_rows(self.S, self.mS, self.vS, self.dS_own, self.adam_s, self.lambda_s,
@@ -234,6 +256,7 @@ class KSlabSolver:
         lo = self.rank * self.chunk
         self.dist.all_gather_into_tensor(self.S_buf, self.S_buf[lo:lo + self.chunk])
         # (the next cpass_nsq rebuilds every slice's ||S_new||^2 partial from the gathered S)
+        self._rs_norm = True
 
     def iteration(self):
         self.c_step()

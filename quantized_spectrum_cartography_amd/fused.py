@@ -97,6 +97,20 @@ class PassEngine:
                   _lib.ptr(mS), _lib.ptr(vS), adam, float(lambda_s), _lib.ptr(self.state),
                   _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
 
+    def spass_kslab(self, S_pos, C, dS_rs, chunk_rows, nranks):
+        """K-slab S-pass (qsc_spass_kslab): the partial dS into the reduce-scatter buffer dS_rs
+        (nranks chunks of chunk_rows rows, each followed by one extra slice holding this slab's
+        ||C||^2 in its first element)."""
+        self.gen += 1
+        o = self.obs
+        u = _lib.QSC_SLICE
+        if chunk_rows % u:
+            raise ValueError("K-slab chunks must be whole position slices")
+        _lib.call("qsc_spass_kslab", self.desc, _lib.ptr(self.s_entries), _lib.ptr(o.s_width),
+                  _lib.ptr(o.s_off), o.model, self.R, _lib.ptr(S_pos), _lib.ptr(C),
+                  _lib.ptr(dS_rs), chunk_rows // u, int(nranks), _lib.ptr(self.state),
+                  _lib.ptr(self.ws), self.ws.numel(), _lib.stream())
+
     def scpass_supported(self):
         return bool(_lib.lib().qsc_scpass_supported(self.desc, self.R))
 

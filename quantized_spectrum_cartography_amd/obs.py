@@ -34,6 +34,16 @@ def default_tile(P, R, K):
         return int(os.environ["QSC_CTILE"])
     Pp = -(-P // 64) * 64
     nks = -(-K // 64)
+    if R <= 8:
+        # the tile-form C-pass and the fused launch run one workgroup per tile: ~256 tiles (one
+        # round on the 256 CUs) whatever K is.  Sizing by tiles x k-slices (the per-slice C-pass
+        # form's rule) gave the K-slab shares of C3 (K_loc = 32, 64) 256-position tiles and 4x
+        # the slab rows to finish: c3k8 C-finish 6.87 us at 256 positions, 3.26 us at 1024, C-pass
+        # 9.81 / 9.57 us (profiles/r06/kslab/c3k8_tiles.log)
+        t = 256
+        while t * 256 < Pp and t < 1024:
+            t *= 2
+        return t
     want = max(1, (Pp * nks) // 1024)
     t = 256
     while t * 2 <= want and t < 1024:
@@ -232,11 +242,15 @@ class Observations:
             self._iperm = ip
         return ip
 
-    def to_positions(self, X):
-        """(R, P) natural pixel order -> (Pp, RP) position order (pixel-major rows, zero padded)."""
+    def to_positions(self, X, out=None):
+        """(R, P) natural pixel order -> (Pp, RP) position order (pixel-major rows, zero padded);
+        into `out` when given (a persistent buffer, e.g. inside a captured hipGraph)."""
         R = X.shape[0]
         Xd = _dev(X.detach().to(torch.float32)).reshape(R, self.P).contiguous()
-        out = torch.empty((self.Pp, self.rank_pad(R)), dtype=torch.float32, device=Xd.device)
+        if out is None:
+            out = torch.empty((self.Pp, self.rank_pad(R)), dtype=torch.float32, device=Xd.device)
+        elif out.shape != (self.Pp, self.rank_pad(R)) or not out.is_contiguous():
+            raise ValueError("out must be a contiguous (%d, %d) tensor" % (self.Pp, self.rank_pad(R)))
         _lib.call("qsc_perm_gather", _lib.ptr(Xd), _lib.ptr(self.perm), R, self.P, self.Pp,
                   _lib.ptr(out), _lib.stream())
         return out

@@ -56,6 +56,8 @@ def issue_iterations(solver, n):
     of run(a + b) -- c_step, fused_body x (a + b - 1), then the last S-step -- and every run of
     n iterations issues n fused launches and n C-step finishes (the steady state), where the
     stand-alone ends cost a C-pass and an S-pass per run."""
+    if hasattr(solver, "begin_run"):
+        solver.begin_run()
     if getattr(solver, "fuse", False) and getattr(solver, "chain", False) and n >= 1:
         if solver.ahead():
             solver.c_finish()
@@ -488,81 +490,290 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
                            nmse=nmse, iters=max_iter, fused=sol.fuse)
     return _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c, lr_s,
                             max_iter, betas, eps, project_c, restart, restart_samples, T_true,
-                            nmse_every, callback)
+                            nmse_every, callback, use_graph=use_graph)
+
+
+# iterations per captured hipGraph of the generator / DIP solver (GeneratorSolver): every
+# iteration is ~100 graph nodes (the torch decoder's forward and backward, its optimizer step and
+# the HIP passes), so long runs replay a chunk graph instead of one graph of the whole run
+GEN_GRAPH_ITERS = 32
+
+
+class GeneratorSolver:
+    """S = generator(Z) alternating solver (qmc/qmc.ipynb :541-634) as a device-resident op
+    sequence that is captured in hipGraphs (the DIP solver of dip.solve, the GAN path of solve).
+
+    One iteration, no host synchronisation anywhere:
+      C-step  fused HIP C-pass at S_pos (the S of the previous S-step, :564) + qsc_cfinish (Adam on
+              C, C >= 0, :576-579); the step's NLL / ||C||^2 stay in the engine's history rows;
+      S-step  S = generator(Z) (torch, MIOpen convs), S -> position order (qsc_perm_gather into
+              the persistent S_pos), fused HIP S-pass in gradient mode (dS), qsc_state_flush
+              (the S-step NLL into the history row), dS -> pixel order, the surrogate
+              <S, dS> + lambda_s ||Z||_F back-propagated through the generator (:626-633), the
+              optimizer step (:634) -- torch Adam with capturable=True, so its step counters
+              live on the device; lambda_s ||Z|| recorded on the device.
+    run(n, use_graph=True) replays captured chunk graphs of GEN_GRAPH_ITERS iterations (sharing
+    one memory pool) after WARMUP eager iterations, which create the optimizer state and the
+    autograd / MIOpen workspaces outside capture.  Graph replay and eager issue run the same
+    kernels on the same buffers, so the results are bitwise equal
+    (tests/test_gpu_fused.py::test_generator_solver_graph_equals_eager).  A capture that fails
+    (a library call that cannot be captured) is recorded in `graph_error` and the solver runs
+    eagerly from then on."""
+
+    WARMUP = 1
+
+    def __init__(self, obs, generator, Z_init, C_init, R, lambda_c=100.0, lambda_s=100.0,
+                 lr_c=5e-3, lr_s=1e-2, betas=(0.9, 0.999), eps=1e-8, project_c=True,
+                 params=None, optimize_z=True, hist_cap=1024):
+        dev = obs.device
+        self.obs, self.net, self.R = obs, generator, R
+        self.I, self.J = obs.I, obs.J
+        self.engine = PassEngine(obs, R, hist_cap=max(int(hist_cap), 1))
+        self.C = _dev(C_init.detach().to(torch.float32)).reshape(R, obs.K).clone()
+        self.mC, self.vC = torch.zeros_like(self.C), torch.zeros_like(self.C)
+        self.adam_c = _lib.make_adam(lr_c, betas, eps, project_nonneg=project_c)
+        self.lambda_c, self.lambda_s = float(lambda_c), float(lambda_s)
+        self.Z = Z_init.detach().to(dev, torch.float32).clone().requires_grad_(bool(optimize_z))
+        self.plist = ([self.Z] if optimize_z else []) + list(params or [])
+        # capturable: the step counters are device tensors, so one captured optimizer step is
+        # valid at every replay (the eager iterations run the same capturable update)
+        self.optS = torch.optim.Adam(self.plist, lr=lr_s, betas=betas, eps=eps,
+                                     capturable=True)
+        with torch.no_grad():
+            S0 = generator(self.Z).reshape(R, 1, self.I, self.J)
+        self.S_pos = obs.to_positions(S0.reshape(R, -1))
+        self.engine.init_state(self.S_pos)
+        self.dS_pos = torch.zeros_like(self.S_pos)
+        self.dS_pix = torch.zeros((R, obs.P), dtype=torch.float32, device=dev)
+        self.hist_cap = self.engine.hist_cap
+        self.zreg = torch.zeros(self.hist_cap, dtype=torch.float32, device=dev)
+        self.ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.S_last = S0.detach()
+        self.done = 0
+        self._eager_done = 0
+        self._graphs = {}
+        self._pool = None
+        self.graph_error = None
+        self.graph_capturable = True
+
+    # ---- one iteration (capturable) -----------------------------------------------------
+    def c_step(self):
+        e = self.engine
+        e.cpass(self.S_pos, self.C)
+        e.cfinish(self.C, 1, mC=self.mC, vC=self.vC, adam=self.adam_c, lambda_c=self.lambda_c)
+
+    def s_step(self):
+        e, R = self.engine, self.R
+        self.optS.zero_grad(set_to_none=False)
+        S = self.net(self.Z).reshape(R, 1, self.I, self.J)
+        self.obs.to_positions(S.detach().reshape(R, -1), out=self.S_pos)
+        e.spass(self.S_pos, self.C, 0, dS=self.dS_pos)
+        e.flush(record=True)  # the S-step NLL -> this iteration's history row
+        self.obs.to_pixels(self.dS_pos, R, out=self.dS_pix)
+        reg = self.lambda_s * torch.norm(self.Z, "fro")
+        surrogate = (S * self.dS_pix.reshape(R, 1, self.I, self.J)).sum() + reg
+        surrogate.backward()
+        self.optS.step()
+        with torch.no_grad():
+            self.zreg.index_copy_(0, self.ctr.clamp(max=self.hist_cap - 1),
+                                  reg.detach().reshape(1))
+            self.ctr += 1
+        self.S_last = S.detach()
+
+    def iteration(self):
+        self.c_step()
+        self.s_step()
+
+    # ---- runs ---------------------------------------------------------------------------
+    def _capture(self, m):
+        g = torch.cuda.CUDAGraph()
+        s = capture_stream()
+        caller = torch.cuda.current_stream()
+        s.wait_stream(caller)
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+        gen0 = self.engine.gen
+        try:
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s, pool=self._pool):
+                    for _ in range(m):
+                        self.iteration()
+        except Exception as e:  # noqa: BLE001 - every failure takes the same clean-up path
+            del g
+            abandon_capture(s, caller)
+            self.engine.gen = gen0
+            self.graph_error = "%s: %s" % (type(e).__name__, e)
+            self.graph_capturable = False
+            warnings.warn("hipGraph capture of the generator iteration failed; running eagerly "
+                          "(%s)" % self.graph_error, RuntimeWarning)
+            return None
+        self.engine.gen = gen0
+        caller.wait_stream(s)
+        _upload(g)
+        return g
+
+    def _graph(self, m):
+        if not self.graph_capturable:
+            return None
+        if m not in self._graphs:
+            self._graphs[m] = self._capture(m)
+        return self._graphs[m]
+
+    def prepare(self, n):
+        """Capture (without executing) the chunk graphs run(n) will replay.  Needs the WARMUP
+        eager iterations done (they create the optimizer state outside capture)."""
+        if self._eager_done < self.WARMUP:
+            raise RuntimeError("prepare() after %d eager iterations (run them first)" % self.WARMUP)
+        for m in sorted(set(_gen_chunks(n))):
+            self._graph(m)
+
+    def run(self, n, use_graph=True):
+        """Enqueue n iterations (no host sync)."""
+        use_graph = use_graph and torch.cuda.is_available() and self.C.is_cuda
+        while n > 0 and (self._eager_done < self.WARMUP or not use_graph):
+            self.iteration()
+            self._eager_done += 1
+            self.done += 1
+            n -= 1
+        for m in _gen_chunks(n):
+            g = self._graph(m)
+            if g is None:
+                for _ in range(m):
+                    self.iteration()
+            else:
+                g.replay()
+            self.done += m
+
+    # ---- results --------------------------------------------------------------------------
+    def S_pixels(self):
+        """The last S-step's generator output S (R, 1, I, J)."""
+        return self.S_last
+
+    def state(self):
+        return self.engine.read_state()
+
+    def history(self):
+        """Per-iteration costs (qmc/qmc.ipynb :573, :631): C-step cost at the C it
+        differentiates, S-step cost at the updated C (both with lambda_s ||Z|| of the S-step's
+        Z), from the device history rows (one synchronisation)."""
+        n = min(self.done, self.hist_cap)
+        h = self.engine.hist[: 4 * n].view(n, 4).double().cpu()
+        z = self.zreg[:n].double().cpu()
+        nsq_c_final = float((self.C.double() ** 2).sum().item())
+        costs_c, costs_s = [], []
+        for i in range(n):
+            nll_c, nll_s, nsq_c = h[i][0].item(), h[i][1].item(), h[i][2].item()
+            nsq_next = h[i + 1][2].item() if i + 1 < n else nsq_c_final
+            costs_c.append(nll_c + self.lambda_c * math.sqrt(nsq_c) + z[i].item())
+            costs_s.append(nll_s + self.lambda_c * math.sqrt(nsq_next) + z[i].item())
+        return costs_c, costs_s
+
+
+def _gen_chunks(n):
+    out = []
+    while n > 0:
+        m = min(n, GEN_GRAPH_ITERS)
+        out.append(m)
+        n -= m
+    return out
 
 
 def _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c, lr_s, max_iter,
                      betas, eps, project_c, restart, restart_samples, T_true, nmse_every,
-                     callback, params=None, optimize_z=True):
-    """S = generator(Z) variant (qmc/qmc.ipynb :541-634).  The S-step optimises Z
-    (optimize_z) plus any extra `params` — the DIP solver passes the decoder weights."""
+                     callback, params=None, optimize_z=True, use_graph=True):
+    """S = generator(Z) variant (qmc/qmc.ipynb :541-634) on a GeneratorSolver.  The S-step
+    optimises Z (optimize_z) plus any extra `params` -- the DIP solver passes the decoder
+    weights.  The one-time random restart of Z (:590-619, i == 1) runs eagerly between the
+    C-step and the S-step of iteration 1; the rest runs as captured hipGraph chunks (use_graph).
+    With `callback` or NMSE tracking the run is split into chunks of `nmse_every` iterations
+    (callback(i, dict(S, C, Z)) after each, S the last S-step's generator output)."""
+    sol = GeneratorSolver(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c, lr_s,
+                          betas, eps, project_c, params=params, optimize_z=optimize_z,
+                          hist_cap=max_iter)
+    return drive_generator(sol, max_iter, restart, restart_samples, T_true, nmse_every, callback,
+                           use_graph)
+
+
+def drive_generator(sol, max_iter, restart=False, restart_samples=(200, 200), T_true=None,
+                    nmse_every=0, callback=None, use_graph=True):
+    """Run a fresh GeneratorSolver for max_iter iterations (the loop of qmc/qmc.ipynb :559-645)
+    and collect its SolveResult."""
+    obs, generator, R = sol.obs, sol.net, sol.R
+    lambda_c, lambda_s = sol.lambda_c, sol.lambda_s
+    nmse = []
+    chunk = max(int(nmse_every), 1) if (callback is not None or (T_true is not None and nmse_every)) \
+        else max_iter
+    done = 0
+
+    def after(k):
+        if T_true is not None and nmse_every and k % nmse_every == 0:
+            nmse.append(map_nmse(sol.S_last, sol.C, T_true))
+        if callback is not None:
+            callback(k, dict(S=sol.S_last, C=sol.C, Z=sol.Z))
+
+    if restart and max_iter >= 2:
+        # iteration 0, then iteration 1's C-step, the restart, and its S-step (eager)
+        sol.run(1, use_graph=False)
+        after(1)
+        sol.c_step()
+        _restart_z(sol, obs, generator, R, lambda_c, lambda_s, restart_samples)
+        sol.s_step()
+        sol._eager_done += 1
+        sol.done += 1
+        after(2)
+        done = 2
+    while done < max_iter:
+        n = min(chunk - (done % chunk), max_iter - done)
+        sol.run(n, use_graph=use_graph)
+        done += n
+        if callback is not None or (T_true is not None and nmse_every):
+            after(done)
+    costs_c, costs_s = sol.history()
+    res = SolveResult(S=sol.S_last, C=sol.C, costs_c=costs_c, costs_s=costs_s, nmse=nmse,
+                      Z=sol.Z.detach(), iters=max_iter)
+    res.graph_error = sol.graph_error
+    res.solver = sol
+    return res
+
+
+def _restart_z(sol, obs, generator, R, lambda_c, lambda_s, restart_samples):
+    """The notebook's one-time random restart of Z at i == 1 (:590-619): 200 random candidates,
+    the best by its full cost, then 200 perturbations of it -- whose cost the reference
+    evaluates at the LAST first-round sample (temp_out, :611: a reference quirk kept as is).
+    Candidates are scored on a separate pass engine (its own state), so the solver's step
+    counters and history rows are untouched."""
     dev = obs.device
     I, J = obs.I, obs.J
     eng = PassEngine(obs, R, hist_cap=0)
-    C = _dev(C_init.detach().to(torch.float32)).reshape(R, obs.K).clone()
-    mC, vC = torch.zeros_like(C), torch.zeros_like(C)
-    adam_c = _lib.make_adam(lr_c, betas, eps, project_nonneg=project_c)
-    Z = Z_init.detach().to(dev, torch.float32).clone().requires_grad_(True)
-    plist = ([Z] if optimize_z else []) + list(params or [])
-    optS = torch.optim.Adam(plist, lr=lr_s, betas=betas, eps=eps)
-    with torch.no_grad():
-        S = generator(Z).reshape(R, 1, I, J)
-    S_pos = obs.to_positions(S.reshape(R, -1))
-    eng.init_state(S_pos)
-    dS_pos = torch.empty_like(S_pos)
-    costs_c, costs_s, nmse = [], [], []
+    Sp = torch.empty_like(sol.S_pos)
+    dSp = torch.empty_like(sol.S_pos)
+    eng.init_state(Sp.zero_())
+    Z = sol.Z
 
     def nll_of(S_cand):
-        Sp = obs.to_positions(S_cand.reshape(R, -1))
-        eng.spass(Sp, C, 0, dS=dS_pos)
+        obs.to_positions(S_cand.reshape(R, -1), out=Sp)
+        eng.spass(Sp, sol.C, 0, dS=dSp)
         eng.flush(record=False)
         return eng.read_state()["nll_s"]
 
-    for i in range(max_iter):
-        # ---- C-step (cost uses the S of the previous S-step, :564) ----
-        nsq_c = float((C.double() ** 2).sum())
-        eng.cpass(S_pos, C)
-        eng.cfinish(C, 1, mC=mC, vC=vC, adam=adam_c, lambda_c=lambda_c)
-        st = eng.read_state()
-        costs_c.append(st["nll_c"] + lambda_c * math.sqrt(nsq_c) + lambda_s * float(torch.norm(Z.detach())))
-        # (cfinish left step_c += 1 pending; the next S-pass applies it)
-        # ---- one-time random restart of Z (:590-619) ----
-        if restart and i == 1:
-            best = float("inf")
-            n1, n2 = restart_samples
-            last = None
-            for _ in range(n1):
-                cand = torch.randn((R, Z.shape[1]), dtype=torch.float32)
-                with torch.no_grad():
-                    out = generator(cand.to(dev)).reshape(R, 1, I, J)
-                crit = nll_of(out) + lambda_c * float(torch.norm(C)) + lambda_s * float(torch.norm(S.detach()))
-                last = out
-                if crit < best:
-                    Z.data = cand.to(dev).clone()
-                    best = crit
-            for _ in range(n2):
-                # the reference re-evaluates the last first-round sample here (temp_out, :611)
-                cand = 0.2 * torch.randn((R, Z.shape[1]), dtype=torch.float32) + Z.detach().cpu()
-                crit = nll_of(last) + lambda_c * float(torch.norm(C)) + lambda_s * float(torch.norm(S.detach()))
-                if crit < best:
-                    Z.data = cand.to(dev).clone()
-                    best = crit
-        # ---- S-step through the generator (:622-634) ----
-        optS.zero_grad()
-        S = generator(Z).reshape(R, 1, I, J)
-        S_pos = obs.to_positions(S.detach().reshape(R, -1))
-        eng.spass(S_pos, C, 0, dS=dS_pos)
-        eng.flush(record=False)
-        dS = obs.to_pixels(dS_pos, R).reshape(R, 1, I, J)
-        reg = lambda_s * torch.norm(Z, "fro")
-        surrogate = (S * dS).sum() + reg
-        surrogate.backward()
-        optS.step()
-        st = eng.read_state()
-        costs_s.append(st["nll_s"] + lambda_c * float(torch.norm(C)) + float(reg.detach()))
-        if T_true is not None and nmse_every and (i + 1) % nmse_every == 0:
-            nmse.append(map_nmse(S.detach(), C, T_true))
-        if callback is not None:
-            callback(i + 1, dict(S=S, C=C, Z=Z))
-    return SolveResult(S=S.detach(), C=C, costs_c=costs_c, costs_s=costs_s, nmse=nmse, Z=Z.detach(),
-                       iters=max_iter)
+    S_now = sol.S_last
+    best = float("inf")
+    n1, n2 = restart_samples
+    last = None
+    for _ in range(n1):
+        cand = torch.randn((R, Z.shape[1]), dtype=torch.float32)
+        with torch.no_grad():
+            out = generator(cand.to(dev)).reshape(R, 1, I, J)
+        crit = nll_of(out) + lambda_c * float(torch.norm(sol.C)) + lambda_s * float(torch.norm(S_now))
+        last = out
+        if crit < best:
+            with torch.no_grad():
+                Z.copy_(cand.to(dev))
+            best = crit
+    for _ in range(n2):
+        cand = 0.2 * torch.randn((R, Z.shape[1]), dtype=torch.float32) + Z.detach().cpu()
+        crit = nll_of(last) + lambda_c * float(torch.norm(sol.C)) + lambda_s * float(torch.norm(S_now))
+        if crit < best:
+            with torch.no_grad():
+                Z.copy_(cand.to(dev))
+            best = crit

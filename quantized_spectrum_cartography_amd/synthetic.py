@@ -306,4 +306,5 @@ CONFIGS = {
     "c3k8": (512, 512, 32, 8),
     # log model (4 log bins, sigma 5) on a generated map, free S (c5_problem)
     "c5": (256, 256, 64, 4),
+    "c5dip": (256, 256, 64, 4),
 }

@@ -127,6 +127,22 @@ class _CpuEngine:
         self._adam(S, mS, vS, gg, self.st["step_s"], adam)
         self.st["normsq_s"] = float((S.double() ** 2).sum())  # this shard's, settled later
 
+    def spass_kslab(self, S, C, dS_rs, chunk_rows, nranks):
+        """qsc_spass_kslab: dS rows into the reduce-scatter layout (nranks chunks of chunk_rows
+        rows, each followed by row_unit extra rows) + ||C_slab||^2 into every extra row's first
+        element"""
+        self.calls.append("spass_kslab")
+        P = S.shape[0]
+        g = torch.empty_like(S)
+        self.spass(S, C, 0, dS=g)
+        u, cn = self.row_unit, float((C.double() ** 2).sum())
+        for c in range(nranks):
+            a, b_ = c * chunk_rows, min((c + 1) * chunk_rows, P)
+            base = c * (chunk_rows + u)
+            if b_ > a:
+                dS_rs[base:base + (b_ - a)] = g[a:b_]
+            dS_rs[base + chunk_rows, 0] = cn
+
     def scpass_supported(self):
         return True
 
@@ -216,6 +232,9 @@ def _run(dist_mod, rank, world, K=K):
     assert eng.calls.count("supdate_rows") == ITERS
     # 4 kernels per iteration: the slices' ||S||^2 ride on the C-pass (no slice_nsq launch)
     assert eng.calls.count("cpass_nsq") == ITERS and "slice_nsq" not in eng.calls[:-1]
+    # the global ||C||^2 rides on the reduce-scatter of dS: one all-reduce per run (its first
+    # C-step), not one per iteration
+    assert eng.calls.count("spass_kslab") == ITERS
     assert sol.r1 - sol.r0 <= -(-I * J // world)
     st = eng.read_state()
     st["shard"] = (sol.r0, sol.r1)

@@ -375,6 +375,74 @@ def test_dip_solver_vs_oracle(optimize, iters):
     assert np.allclose(res.costs_s, ref["costs_s"], rtol=1e-4)
 
 
+def _dip256_case(R=4, K=64, N=256, seed=3):
+    """A C5-shaped DIP problem (256 x 256, K = 64, log model, 4 log bins, sigma 5, f = 0.1) with
+    a BN-calibrated SizedDecoderDip -- the decoder dip.solve builds for config 5."""
+    from quantized_spectrum_cartography_amd import dip, nets
+    from quantized_spectrum_cartography_amd.utils import LOG_OFFSET_4, QUANTIZATION_BOUNDARIES_4_BINS_LOG
+    torch.manual_seed(seed)
+    dec = nets.SizedDecoderDip(N, 256)
+    Z0 = torch.randn(R, 256)
+    dip.calibrate_bn(dec, Z0)
+    S_true = torch.rand(R, 1, N, N) ** 4 * 0.2
+    C_true = torch.rand(R, K)
+    Tt = ro.get_tensor(S_true, C_true)
+    b = torch.tensor(QUANTIZATION_BOUNDARIES_4_BINS_LOG)
+    Y = ro.quantize(Tt, 5.0, b, offset=LOG_OFFSET_4, log_model=True).unsqueeze(1)
+    Wx = torch.bernoulli(torch.full((K, 1, N, N), 0.1))
+    C0 = 0.05 * torch.rand(R, K)
+    return dec, Z0, C0, Y, Wx, b, LOG_OFFSET_4
+
+
+def test_dip_solver_256_vs_oracle_graph():
+    """VERDICT r5 missing 3: dip.solve at config 5's size (256 x 256, K = 64, R = 4, the 256^2
+    SizedDecoderDip), z-mode, end to end vs the oracle's reference-formulation loop
+    (oracle/solver.py dip_solve, CPU autograd) at 1e-4 -- through the captured-hipGraph path
+    (one eager iteration, then graph replays of the decoder forward / backward, its Adam step
+    and the fused HIP passes)."""
+    import copy
+    from quantized_spectrum_cartography_amd import dip
+    dec, Z0, C0, Y, Wx, b, off = _dip256_case()
+    iters = 5
+    ref = osolver.dip_solve(copy.deepcopy(dec).eval(), Z0, C0, Y, Wx, b, 5.0, off, True,
+                            n_iter=iters, lr_s=1e-2, optimize="z")
+    res = dip.solve(Y, Wx, b, 5.0, 4, offset=off, decoder=copy.deepcopy(dec).cuda(), Z_init=Z0,
+                    C_init=C0, max_iter=iters, lr_s=1e-2, optimize="z", use_graph=True)
+    assert res.graph_error is None, res.graph_error
+    assert len(res.solver._graphs) == 1  # the iterations after the first were graph replays
+    assert rel_fro(res.S.cpu().numpy(), ref["S"].numpy()) < 1e-4
+    assert rel_fro(res.C.cpu().numpy(), ref["C"].numpy()) < 1e-4
+    assert np.allclose(res.costs_c, ref["costs_c"], rtol=1e-4)
+    assert np.allclose(res.costs_s, ref["costs_s"], rtol=1e-4)
+
+
+@pytest.mark.parametrize("optimize", ["z", "weights"])
+def test_generator_solver_graph_equals_eager(optimize):
+    """GeneratorSolver: the captured-hipGraph run (chunk graphs after one eager iteration) and
+    the eager op sequence give the same S, C, Z and costs bit for bit (same kernels on the same
+    buffers), at C5's size with the 256^2 decoder."""
+    import copy
+    from quantized_spectrum_cartography_amd import dip, qmc
+    dec, Z0, C0, Y, Wx, b, off = _dip256_case(seed=4)
+    old = qmc.GEN_GRAPH_ITERS
+    qmc.GEN_GRAPH_ITERS = 4  # two chunk graphs (4 + 2) after the eager iteration
+    try:
+        out = []
+        for g in (False, True):
+            r = dip.solve(Y, Wx, b, 5.0, 4, offset=off, decoder=copy.deepcopy(dec).cuda(),
+                          Z_init=Z0, C_init=C0, max_iter=7, lr_s=1e-3, optimize=optimize,
+                          use_graph=g)
+            out.append(r)
+    finally:
+        qmc.GEN_GRAPH_ITERS = old
+    a, c = out
+    assert c.graph_error is None and len(c.solver._graphs) == 2
+    assert np.array_equal(a.S.cpu().numpy(), c.S.cpu().numpy())
+    assert np.array_equal(a.C.cpu().numpy(), c.C.cpu().numpy())
+    assert np.array_equal(a.Z.cpu().numpy(), c.Z.cpu().numpy())
+    assert a.costs_c == c.costs_c and a.costs_s == c.costs_s
+
+
 def test_dip_solver_256():
     from quantized_spectrum_cartography_amd import dip
     from quantized_spectrum_cartography_amd.utils import QUANTIZATION_BOUNDARIES_4_BINS_LOG
