@@ -283,18 +283,10 @@ QSC_API int qsc_obs_fill(const uint8_t* codes, const qsc_obs_desc* desc, const i
  * group has <= W entries of that residue).  Blocks with lists longer than 256 keep their order.
  * SYNCHRONOUS (reads the longest list width); run once per packing, after qsc_obs_fill. */
 QSC_API size_t qsc_obs_schedule_workspace_bytes(const qsc_obs_desc* desc);
-/* c_split (nullable, qsc_obs_split): C-format blocks keep each lane's first 4*c_split entries
- * in its first 4*c_split slots (the two slot ranges are ordered separately). */
 QSC_API int qsc_obs_schedule(const qsc_obs_desc* desc, const int32_t* s_width,
                              const int64_t* s_off, const int32_t* c_width, const int64_t* c_off,
-                             const int32_t* c_split, void* s_entries, void* c_entries, void* ws,
-                             size_t ws_bytes, void* stream);
-/* Phase split of the naturally ordered C-format lists for qsc_scpass: c_split[block] = min over
- * the block's lanes that hold entries of floor(n0 / 4), n0 = the lane's entries with tile row
- * < split_rows (async).  Run after qsc_obs_fill, before qsc_obs_schedule. */
-QSC_API int qsc_obs_split(const qsc_obs_desc* desc, const int32_t* c_width, const int64_t* c_off,
-                          const void* c_entries, int32_t split_rows, int32_t* c_split,
-                          void* stream);
+                             void* s_entries, void* c_entries, void* ws, size_t ws_bytes,
+                             void* stream);
 /* Host (CPU) form of one group's schedule, the same code as the device pass (tests / tools):
  * in/out are 16 lists of W uint32 entry values, lane-major; rowfmt/rows/wide describe the
  * entry values as in qsc_obs_desc (rows = K for S-format lists, PT for C-format lists).
@@ -353,18 +345,12 @@ QSC_API int qsc_cpass(const qsc_obs_desc* d, const void* c_entries, const int32_
  * followed by qsc_cpass at the updated S -- same partials, same state protocol -- so a solver
  * runs  cpass, cfinish, (scpass, cfinish) x (n-1), spass  for n outer iterations
  * (qmc/qmc.ipynb :562-634).  One workgroup per C-pass pixel tile: the tile's S-step results
- * feed its C-pass through LDS.  Available when qsc_scpass_supported(d, R).
- * Phase split (optional): c_split[ntiles*nks] from qsc_obs_split(split_rows) with split_rows ==
- * qsc_scpass_split_rows(d, R) (0: no split at this rank) lets each C-pass unit walk its chunks
- * j < c_split[block] right after the launch's first S-step round -- those chunks hold only the
- * tile rows that round updated -- overlapping C-pass arithmetic with the rest of the S-step's
- * HBM traffic; the sums and their order are unchanged.  c_split == NULL: no split. */
+ * feed its C-pass through LDS.  Available when qsc_scpass_supported(d, R). */
 QSC_API int qsc_scpass_supported(const qsc_obs_desc* d, int32_t R);
-QSC_API int32_t qsc_scpass_split_rows(const qsc_obs_desc* d, int32_t R);
 QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
                        const int64_t* s_off, const void* c_entries, const int32_t* c_width,
-                       const int64_t* c_off, const int32_t* c_kmap, const int32_t* c_split,
-                       int32_t split_rows, const qsc_model* m, int32_t R, float* S,
+                       const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
+                       int32_t R, float* S,
                        const float* C, float* mS, float* vS, const qsc_adam* adam,
                        float lambda_s, qsc_state* st, void* ws, size_t ws_bytes, void* stream);
 /* reduce the C-pass slab (fixed order).  mode 0: write dC (NLL gradient only); mode 1: fused

@@ -105,10 +105,12 @@ def _threads():
 
 def nll_grad_obs(S, C, obs, b, sigma, offset=0.0, log_model=False, chunk=1 << 20, threads=None):
     """nll_grad restricted to observed entries obs = (kk, pp, yy): identical math (fp64),
-    evaluated in chunks of `chunk` entries (bounded host memory) on a thread pool (numpy
-    releases the GIL in its loops), so C4's 27 M entries take seconds.  The NLL is summed in
-    chunk order and the gradients are per-factor bincounts: the result does not depend on the
-    thread count."""
+    evaluated in chunks of `chunk` entries on a thread pool (numpy releases the GIL in its
+    loops), so C4's 27 M entries take seconds.  Each chunk returns its NLL and its per-factor
+    bincounts of the gradient (R x P and R x K), summed in chunk order: the result does not
+    depend on the thread count, and host memory stays bounded by chunk-sized temporaries plus
+    one R x (P + K) partial per chunk (per-factor tasks over all entries held two
+    nnz-sized fp64 arrays each, ~7 GB at C4 with 16 threads)."""
     from concurrent.futures import ThreadPoolExecutor
     S = np.asarray(S, np.float64)
     C = np.asarray(C, np.float64)
@@ -118,7 +120,6 @@ def nll_grad_obs(S, C, obs, b, sigma, offset=0.0, log_model=False, chunk=1 << 20
     ST, CT = np.ascontiguousarray(S.T), np.ascontiguousarray(C.T)  # row gathers
     e = edges_of(b, log_model)
     a = sigma * 1.414213
-    g = np.empty(kk.shape[0], np.float64)
 
     def one(i0):
         k, p, y = kk[i0:i0 + chunk], pp[i0:i0 + chunk], yy[i0:i0 + chunk]
@@ -130,19 +131,19 @@ def nll_grad_obs(S, C, obs, b, sigma, offset=0.0, log_model=False, chunk=1 << 20
         with np.errstate(divide="ignore", invalid="ignore"):
             part = -float(np.sum(np.log(Pr)))
             gx = (np.exp(-u * u) - np.exp(-w * w)) / (a * math.sqrt(math.pi) * Pr)
-        g[i0:i0 + chunk] = gx * (1.0 / (t + offset) if log_model else 1.0)
-        return part
+        g = gx * (1.0 / (t + offset) if log_model else 1.0)
+        # dS[r, p] = sum_k g C[r, k];  dC[r, k] = sum_p g S[r, p]  (this chunk's terms)
+        dSc = np.stack([np.bincount(p, weights=g * CT[k, r], minlength=P) for r in range(R)])
+        dCc = np.stack([np.bincount(k, weights=g * ST[p, r], minlength=K) for r in range(R)])
+        return part, dSc, dCc
 
     nth = threads or _threads()
+    nll, dS, dC = 0.0, np.zeros((R, P)), np.zeros((R, K))
     with ThreadPoolExecutor(nth) as ex:
-        nll = 0.0
-        for part in ex.map(one, range(0, kk.shape[0], chunk)):
+        for part, dSc, dCc in ex.map(one, range(0, kk.shape[0], chunk)):
             nll += part
-        # dS[r, p] = sum_k g C[r, k];  dC[r, k] = sum_p g S[r, p]
-        dS = np.stack(list(ex.map(lambda r: np.bincount(pp, weights=g * C[r, kk], minlength=P),
-                                  range(R))))
-        dC = np.stack(list(ex.map(lambda r: np.bincount(kk, weights=g * S[r, pp], minlength=K),
-                                  range(R))))
+            dS += dSc
+            dC += dCc
     return nll, dS, dC
 
 

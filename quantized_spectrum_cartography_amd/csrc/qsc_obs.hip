@@ -149,8 +149,7 @@ template <typename E>
 __global__ void __launch_bounds__(64) sched_kernel(const E* __restrict__ in, E* __restrict__ out,
                                                    const int* __restrict__ width,
                                                    const int64_t* __restrict__ off, int lanes,
-                                                   int Wcap, SchedFmt f,
-                                                   const int* __restrict__ split) {
+                                                   int Wcap, SchedFmt f) {
   extern __shared__ __attribute__((aligned(16))) char scratch[];
   const int groups = lanes / kSchedLanes;
   const int li = blockIdx.x / groups, g = blockIdx.x - li * groups;
@@ -160,59 +159,15 @@ __global__ void __launch_bounds__(64) sched_kernel(const E* __restrict__ in, E* 
   auto slot = [&](int i, int j) -> int64_t {
     return base + (int64_t)(j >> 2) * (lanes * 4) + b128_group_lane(g, i) * 4 + (j & 3);
   };
-  // split blocks (C-format, qsc_obs_split): slots [0, 4m) and [4m, W) are ordered separately,
-  // so the first 4m slots of every lane keep its first 4m (natural-order) entries
-  const int Wa = split ? 4 * split[li] : 0;
   bool ok = true;
-  if (Wa > 0) {
+  if (W > 0) {
     auto get = [&](int i, int j) -> uint32_t { return (uint32_t)in[slot(i, j)]; };
     auto put = [&](int i, int c, uint32_t v) { out[slot(i, c)] = (E)v; };
-    ok = Wa <= Wcap && sched_group(scratch, Wa, f, get, put);
-  }
-  if (ok && W > Wa) {
-    auto get = [&](int i, int j) -> uint32_t { return (uint32_t)in[slot(i, Wa + j)]; };
-    auto put = [&](int i, int c, uint32_t v) { out[slot(i, Wa + c)] = (E)v; };
-    ok = (W - Wa) <= Wcap && sched_group(scratch, W - Wa, f, get, put);
+    ok = W <= Wcap && sched_group(scratch, W, f, get, put);
   }
   if (ok) return;
   for (int i = 0; i < kSchedLanes; ++i)
     for (int j = 0; j < W; ++j) out[slot(i, j)] = in[slot(i, j)];
-}
-
-// Phase split of the C-format lists for the fused S-step + C-pass launch (qsc_scpass): per
-// (tile, k-slice) block, m = min over the lanes that hold entries of floor(n0 / 4), n0 = the
-// lane's entries whose tile row is < split_rows.  In natural (ascending) order the first 4m
-// entries of every list are then rows the launch has updated after its first S-step round, so
-// chunks j < m can be evaluated while the rest of the tile's S-step is still running.
-template <typename E>
-__global__ void __launch_bounds__(64) split_kernel(const E* __restrict__ ent,
-                                                   const int* __restrict__ width,
-                                                   const int64_t* __restrict__ off, int nblocks,
-                                                   int split_rows, int sr, int qo, int bits,
-                                                   int* __restrict__ split) {
-  const int li = blockIdx.x, lane = threadIdx.x;
-  if (li >= nblocks) return;
-  const int W = width[li];
-  const int64_t base = off[li];
-  const SchedFmt f = sched_fmt<E>(sr, qo);
-  int n0 = 0, n = 0;
-  for (int j = 0; j < W; ++j) {
-    const uint32_t e = (uint32_t)ent[base + (int64_t)(j >> 2) * 256 + lane * 4 + (j & 3)];
-    if (f.is_pad(e)) continue;
-    ++n;
-    const uint32_t q = sr ? (e >= (uint32_t)sr_off(qo) ? e - (uint32_t)sr_off(qo) : e)
-                          : (e & ((1u << bits) - 1u));
-    n0 += q < (uint32_t)split_rows;
-  }
-  // min over the lanes with entries (wave reduction through LDS: one wave per block)
-  __shared__ int sm[64];
-  sm[lane] = n > 0 ? (n0 >> 2) : 0x7FFFFFFF;
-  __syncthreads();
-  if (lane == 0) {
-    int m = 0x7FFFFFFF;
-    for (int i = 0; i < 64; ++i) m = min(m, sm[i]);
-    split[li] = m == 0x7FFFFFFF ? 0 : m;
-  }
 }
 
 __global__ void width_max_kernel(const int* __restrict__ w, int n, int* __restrict__ out) {
@@ -487,31 +442,9 @@ QSC_API size_t qsc_obs_schedule_workspace_bytes(const qsc_obs_desc* d) {
   return align_up((size_t)std::max(d->s_entries, d->c_entries) * eb) + 256;
 }
 
-QSC_API int qsc_obs_split(const qsc_obs_desc* d, const int32_t* c_width, const int64_t* c_off,
-                          const void* c_entries, int32_t split_rows, int32_t* c_split,
-                          void* stream) {
-  if (!d || !c_width || !c_off || !c_entries || !c_split || split_rows < 0 ||
-      (d->rowfmt != 0 && d->rowfmt != 1))
-    return QSC_EINVAL;
-  const int nb = d->ntiles * d->nks;
-  if (nb < 1) return QSC_OK;
-  hipStream_t s = STREAM(stream);
-  if (d->wide)
-    hipLaunchKernelGGL(split_kernel<uint32_t>, dim3((unsigned)nb), dim3(64), 0, s,
-                       (const uint32_t*)c_entries, c_width, c_off, nb, split_rows, 0, d->PT,
-                       EntryTraits<uint32_t>::kBits, c_split);
-  else
-    hipLaunchKernelGGL(split_kernel<uint16_t>, dim3((unsigned)nb), dim3(64), 0, s,
-                       (const uint16_t*)c_entries, c_width, c_off, nb, split_rows,
-                       d->rowfmt == 1 ? 1 : 0, d->PT, EntryTraits<uint16_t>::kBits, c_split);
-  QSC_CHECK_LAUNCH();
-  return QSC_OK;
-}
-
 QSC_API int qsc_obs_schedule(const qsc_obs_desc* d, const int32_t* s_width, const int64_t* s_off,
-                             const int32_t* c_width, const int64_t* c_off,
-                             const int32_t* c_split, void* s_entries, void* c_entries, void* ws,
-                             size_t ws_bytes, void* stream) {
+                             const int32_t* c_width, const int64_t* c_off, void* s_entries,
+                             void* c_entries, void* ws, size_t ws_bytes, void* stream) {
   if (!d || !s_width || !s_off || !c_width || !c_off || !s_entries || !c_entries || !ws ||
       ws_bytes < qsc_obs_schedule_workspace_bytes(d) || (d->rowfmt != 0 && d->rowfmt != 1))
     return QSC_EINVAL;
@@ -541,15 +474,12 @@ QSC_API int qsc_obs_schedule(const qsc_obs_desc* d, const int32_t* s_width, cons
     QSC_TRY(hipMemcpyAsync(copy, ent, (size_t)n * eb, hipMemcpyDeviceToDevice, s));
     const dim3 grid((unsigned)((int64_t)nl * (lanes / kSchedLanes)));
     const size_t shm = sched_scratch_bytes(wcap);
-    const int* split = fmt == 1 ? c_split : nullptr;
     if (d->wide)
       hipLaunchKernelGGL(sched_kernel<uint32_t>, grid, dim3(64), shm, s, (const uint32_t*)copy,
-                         (uint32_t*)ent, width, off, lanes, wcap, sched_fmt<uint32_t>(0, rows),
-                         split);
+                         (uint32_t*)ent, width, off, lanes, wcap, sched_fmt<uint32_t>(0, rows));
     else
       hipLaunchKernelGGL(sched_kernel<uint16_t>, grid, dim3(64), shm, s, (const uint16_t*)copy,
-                         (uint16_t*)ent, width, off, lanes, wcap, sched_fmt<uint16_t>(sr, rows),
-                         split);
+                         (uint16_t*)ent, width, off, lanes, wcap, sched_fmt<uint16_t>(sr, rows));
     QSC_CHECK_LAUNCH();
   }
   return QSC_OK;

@@ -56,17 +56,12 @@ constexpr int kFBlock = 1024;  // C finish: 16 waves split the tile sum
 #ifndef QSC_EARLY_WAVES
 #define QSC_EARLY_WAVES 16
 #endif
-// fused launch: the other waves read their first slice right after their staging (1) or after
-// the staging barrier (0)
-#ifndef QSC_LATE_LOADS
-#define QSC_LATE_LOADS 0
-#endif
-// fair wave priorities: a wave lowers its s_setprio level as it progresses (S-step: per slice,
-// or with 2 per half slice; C-pass walks: per quarter of the unit's chunk range), so the SIMD
+// fair wave priorities: a wave lowers its s_setprio level as it progresses (S-step: per slice;
+// C-pass walks: per quarter of the unit's chunk range), so the SIMD
 // arbiter, oldest-first among equal levels, keeps the waves of a SIMD abreast instead of
 // finishing them one after another (the last wave of a phase otherwise runs alone,
 // latency-bound: profiles/r05/stamps_simd.log).  A/B at C3: fused launch -0.5 us
-// (profiles/r05/ab_fair_prio.log)
+// (profiles/r05/ab_fair_prio.log; a per-half-slice variant was within noise and is removed)
 #ifndef QSC_FAIR_PRIO
 #define QSC_FAIR_PRIO 1
 #endif
@@ -89,13 +84,11 @@ __device__ __forceinline__ void prio_level(int lvl) {  // 3 = most urgent
 #ifndef QSC_ROW_PF_C
 #define QSC_ROW_PF_C 1
 #endif
-// fused launch at rank <= 8: waves per workgroup (16: 128 VGPRs each; 12: 168, 3 per SIMD) and
-// the software-pipelined S-step gather (signed rows), which needs the larger register budget
+// fused launch at rank <= 8: waves per workgroup (16: 128 VGPRs each; 12: 168, 3 per SIMD --
+// slower, profiles/r05/ab_twelve_waves.log, with or without a software-pipelined S-step gather,
+// which is removed: at 16 waves it spills)
 #ifndef QSC_FUSED_WAVES
 #define QSC_FUSED_WAVES 16
-#endif
-#ifndef QSC_ROW_PF_S
-#define QSC_ROW_PF_S 0
 #endif
 // fused launch: C^T staged from 16-B reads; part-sum bins read at the start
 #ifndef QSC_CT_VEC
@@ -109,22 +102,10 @@ __device__ __forceinline__ void prio_level(int lvl) {  // 3 = most urgent
 #ifndef QSC_SR_SKIP_EDGES
 #define QSC_SR_SKIP_EDGES 1
 #endif
-// fused launch: the phase split (scfused, section 3).  Off by default: its phase-A walk sits
-// between the first S-step round and the rest with the next slice's reads in flight, and at
-// 128 VGPRs (16 waves per CU) that spills (24-115 VGPRs across the instantiations); unsplit,
-// the rank-8 kernels allocate <= 128 with none
-#ifndef QSC_PHASE_SPLIT
-#define QSC_PHASE_SPLIT 0
-#endif
-// C-pass parts: part p of np walks a contiguous block of its list's chunks, or (strided, which
-// the phase split needs) chunks p, p + np, ...; every C-pass form uses the one partition, so
-// their sums agree bit for bit
-#ifndef QSC_STRIDED_PARTS
-#define QSC_STRIDED_PARTS QSC_PHASE_SPLIT
-#endif
-#if QSC_PHASE_SPLIT && !QSC_STRIDED_PARTS
-#error "the phase split needs strided C-pass parts"
-#endif
+// C-pass parts: part p of np walks a contiguous block of its list's chunks; every C-pass form
+// uses the one partition, so their sums agree bit for bit.  (Round 3's phase split of the fused
+// launch -- C-pass chunks of the first S-step round's rows walked between the S-step rounds,
+// which needed strided parts -- spilled at 128 VGPRs and ran slower; removed in round 6.)
 #ifndef QSC_CPASS_WAVES
 #define QSC_CPASS_WAVES 4
 #endif
@@ -132,8 +113,7 @@ struct PartRange {
   int j0, j1, js;  // chunks j0, j0 + js, ... < j1
 };
 __device__ inline PartRange part_range(int W4, int p, int np) {
-  return QSC_STRIDED_PARTS ? PartRange{p, W4, np}
-                           : PartRange{(W4 * p) / np, (W4 * (p + 1)) / np, 1};
+  return PartRange{(W4 * p) / np, (W4 * (p + 1)) / np, 1};
 }
 template <int RP, int W>
 struct Occ {
@@ -698,77 +678,20 @@ __device__ __forceinline__ void walk_groups(const typename Ent<E>::V4* __restric
 // read ahead unconditionally (clamped to the last row: static vmcnt accounting).
 constexpr int kGroupS = 8;
 
-template <int RP, typename E, int KIND, bool LOG, bool PF = false>
+template <int RP, typename E, int KIND, bool LOG>
 __device__ __forceinline__ void walk_halves(const typename Ent<E>::V2* __restrict__ src,
                                             uint32_t lo, int row, int j1,
                                             typename Ent<E>::V2 (&b)[kGroupS],
                                             const f2v (&own)[RP / 2],
                                             const float* __restrict__ tab,
                                             const float2* __restrict__ edges, const Lik& lk,
-                                            f2v (&acc)[RP / 2], f2v& nll, int prio_top = -1) {
+                                            f2v (&acc)[RP / 2], f2v& nll) {
   using V2 = typename Ent<E>::V2;
   j1 = __builtin_amdgcn_readfirstlane(j1);
   const int jlast = max(j1 - 1, 0);
   int jb = 0;
   const uint32_t off = sr_addr<E, KIND>() ? lds_off(tab) : 0u;
-  // (QSC_FAIR_PRIO >= 2, prio_top >= 0: the wave's level drops from prio_top to prio_top - 1
-  // half-way through the slice)
-  auto fair = [&]() {
-    if (QSC_FAIR_PRIO >= 2 && prio_top >= 0) prio_level(prio_top - (2 * jb >= j1 ? 1 : 0));
-  };
-  if constexpr (PF && is_sr(KIND)) {
-    // software-pipelined gather (signed rows): the LDS rows of the next half chunk are read
-    // before the current one's arithmetic, so the gather latency runs under it.  Every buffered
-    // half chunk is a clamped, valid entry, so a read-ahead past the list end is harmless.
-    f2v ra[RP / 2], rb[RP / 2], tra, trb;
-    {
-      uint32_t e[2];
-      ent_rows2<RP, E, KIND>(b[0], off, e);
-      pair_rows<RP, E, KIND, 0>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
-    }
-    for (;;) {
-      fair();
-      const int jn = jb + kGroupS;
-      const bool more = jn < j1;
-      V2 nb[kGroupS];
-#pragma unroll
-      for (int i = 0; i < kGroupS; ++i)
-        nb[i] = ld_lane(src + (int64_t)min(jn + i, jlast) * row, lo);
-#pragma unroll
-      for (int i = 0; i < kGroupS; i += 2)
-        if (jb + i < j1) {
-          uint32_t e[2], f[2];
-          ent_rows2<RP, E, KIND>(b[i], off, e);
-          ent_rows2<RP, E, KIND>(b[i + 1], off, f);
-          f2v xa[RP / 2], xb[RP / 2], txa, txb, pa, pb = splat2(1.0f);
-          pair_rows<RP, E, KIND, 0>(f[0], f[1], own, tab, xa, xb, txa, txb, lk);
-          pair_math<RP, E, KIND, LOG>(e[0], e[1], own, ra, rb, tra, trb, edges, lk, acc, nll, pa,
-                                      true);
-          if (i + 2 < kGroupS) {
-            uint32_t g[2];
-            ent_rows2<RP, E, KIND>(b[i + 2], off, g);
-            pair_rows<RP, E, KIND, 0>(g[0], g[1], own, tab, ra, rb, tra, trb, lk);
-          }
-          if (jb + i + 1 < j1)
-            pair_math<RP, E, KIND, LOG>(f[0], f[1], own, xa, xb, txa, txb, edges, lk, acc, nll,
-                                        pb, true);
-          const f2v pp = pa * pb;
-          nll.x -= __builtin_amdgcn_logf(pp.x * pp.y);
-        }
-      if (!more) break;
-#pragma unroll
-      for (int i = 0; i < kGroupS; ++i) b[i] = nb[i];
-      {
-        uint32_t e[2];
-        ent_rows2<RP, E, KIND>(b[0], off, e);
-        pair_rows<RP, E, KIND, 0>(e[0], e[1], own, tab, ra, rb, tra, trb, lk);
-      }
-      jb = jn;
-    }
-    return;
-  }
   for (;;) {
-    fair();
     const int jn = jb + kGroupS;
     const bool more = jn < j1;
     V2 nb[kGroupS];
@@ -1651,7 +1574,7 @@ struct FusedBlock {
       float *__restrict__ mS, float *__restrict__ vS, qsc_adam ad, float lambda_s,                \
       qsc_state *__restrict__ st, float *__restrict__ part_nll_s, float *__restrict__ part_nsq_s, \
       float *__restrict__ slab, float *__restrict__ part_nll_c, float *__restrict__ cnsq,         \
-      AdamCache *__restrict__ acache, const int *__restrict__ c_split
+      AdamCache *__restrict__ acache
 #define QSC_SCF_KPARAMS                                                                        \
   const E *__restrict__ s_ent, const int *__restrict__ s_width, const int64_t *__restrict__ s_off, \
       const E *__restrict__ c_ent, const int *__restrict__ c_width,                                \
@@ -1661,10 +1584,10 @@ struct FusedBlock {
       float *__restrict__ mS, float *__restrict__ vS, qsc_adam ad, float lambda_s,                \
       qsc_state *__restrict__ st, float *__restrict__ part_nll_s, float *__restrict__ part_nsq_s, \
       float *__restrict__ slab, float *__restrict__ part_nll_c, float *__restrict__ cnsq,         \
-      AdamCache *__restrict__ acache, const int *__restrict__ c_split
+      AdamCache *__restrict__ acache
 #define QSC_SCF_ARGS                                                                            \
   s_ent, s_width, s_off, c_ent, c_width, c_off, c_kmap, nks, NP, PT, lk, E_, nbins, R, K, S, C, mS, \
-      vS, ad, lambda_s, st, part_nll_s, part_nsq_s, slab, part_nll_c, cnsq, acache, c_split
+      vS, ad, lambda_s, st, part_nll_s, part_nsq_s, slab, part_nll_c, cnsq, acache
 
 
 // One pixel tile t of nt of the fused launch (scfused_kernel: t = the workgroup).  C is
@@ -1832,22 +1755,16 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     }
     STAMP(wg, 11);  // (wave 0: the scalars are set)
   };
+  // (late waves' first reads right after their own staging instead of after the barrier:
+  // within noise, round 5, gpurun_out/r05q; not kept)
   if (early) {
     slice_load(cur, s_ent, s_width, s_off, global_of(il < nsl ? il : 0), ln, S, mS, vS);
     stage();
   } else {
     stage();
-#if QSC_LATE_LOADS
-    // (after this wave's C^T reads have landed -- the staging waited for them -- so they are
-    // not queued behind the late waves' slice data; before the barrier, so that data streams
-    // in while the oldest waves compute)
-    slice_load(cur, s_ent, s_width, s_off, global_of(il < nsl ? il : 0), ln, S, mS, vS);
-#endif
   }
   __syncthreads();
-#if !QSC_LATE_LOADS
   if (!early) slice_load(cur, s_ent, s_width, s_off, global_of(il < nsl ? il : 0), ln, S, mS, vS);
-#endif
   STAMP(wg, 1);
   if (t == 0) {
     // ||C_i||^2 for the next C update's regulariser, from the staged C^T at the start (as a
@@ -1871,7 +1788,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     const int il1 = local_of(n + 1);
     const bool more = il1 < nsl;
     const int s = global_of(il);
-#if QSC_FAIR_PRIO == 1
+#if QSC_FAIR_PRIO
     prio_level(3 - min(3, n));  // (uniform: the wave's n-th slice)
 #endif
 #if QSC_FIRST_WAIT
@@ -1894,12 +1811,8 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
     f2v nll = splat2(0.0f);
-    walk_halves<RP, E, KIND, LOG, (QSC_ROW_PF_S != 0) && RP <= 8>(c.src, ln.ent, 2 * QSC_SLICE,
-                                                                   c.j1, c.buf, own, Cl, El, lk,
-                                                                   accp, nll,
-                                                                   QSC_FAIR_PRIO >= 2
-                                                                       ? max(3 - 2 * n, 1)
-                                                                       : -1);
+    walk_halves<RP, E, KIND, LOG>(c.src, ln.ent, 2 * QSC_SLICE, c.j1, c.buf, own, Cl, El, lk,
+                                  accp, nll);
     float acc[RP];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) {
@@ -1936,34 +1849,22 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
     return more;
   };
   // 3. C-pass units of the tile at the new S (cpass_tile_kernel steps 1, 3, 4).
-  //
-  // Phase split (c_split, qsc_obs_split; NP > 1, one C-pass unit per wave, >= 2 S-step rounds):
-  // the first S-step round updates tile rows [0, NW*QSC_SLICE), and every list's chunks j < m
-  // hold only such rows, so right after that round each wave walks its unit's chunks < m
-  // (phase A; the partial dC goes to the unit's part-sum slot in LDS, the NLL pair stays in
-  // registers) while the later rounds' slice reads are in flight, and after the last round the
-  // chunks >= m (phase B), continuing the same accumulators: the same sums in the same order as
-  // the unsplit walk, part of the C-pass arithmetic overlapping the S-step's HBM traffic.
-  const bool split =
-      QSC_PHASE_SPLIT && c_split != nullptr && NP > 1 && U <= NW && nsl >= 2 * NW && 2 * NP <= R;
   int u = w;
   V4 buf[kGroup];
   float cv[RP];
   int wi = 0, jb = 0, je = 0, js = 1, k = 0;
   const V4* src = nullptr;
   const uint32_t lo = (uint32_t)lane * (uint32_t)sizeof(V4);
-  // unit uu: its list block, first chunk jb and end je of this walk (phase 0: whole list;
-  // 1: chunks < m; 2: chunks >= m), the read-ahead of its first chunk group, its bin and C
-  auto unit_begin = [&](int uu, int phase) {
+  // unit uu: its list block and chunk range, the read-ahead of its first chunk group, its bin
+  // and C column
+  auto unit_begin = [&](int uu) {
     const int ks = uu / NP, part = uu - ks * NP;
     wi = t * nks + ks;
     const int W4 = c_width[wi] >> 2;
-    const int m = phase ? min(c_split[wi], W4) : 0;
     const PartRange pr = part_range(W4, part, NP);
     jb = pr.j0;
-    je = phase == 1 ? m : pr.j1;
+    je = pr.j1;
     js = pr.js;
-    if (phase == 2) jb = part + ((max(m - part, 0) + NP - 1) / NP) * NP;  // (strided parts)
     src = reinterpret_cast<const V4*>(c_ent + c_off[wi]);
     QSC_DCHECK(c_off[wi] + (int64_t)c_width[wi] * 64 <= lk.dbg_ent[1]);
     load_group(src, lo, 64, jb, js, max(pr.j1 - 1, 0), buf);
@@ -1972,21 +1873,16 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
 #pragma unroll
     for (int r = 0; r < RP; ++r) cv[r] = Cl[min(k, K - 1) * CP + r];  // C_i, as the S-step used
   };
-  // the walk of the current unit from accumulators acc (zero, or phase A's partial in Pl)
   f2v cnll = splat2(0.0f);
-  auto unit_walk = [&]<bool PFC = (QSC_ROW_PF_C != 0)>(bool from_pl, f2v (&accp)[RP / 2]) {
+  auto unit_walk = [&](f2v (&accp)[RP / 2]) {
     f2v own[RP / 2];
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j)
       own[j] = f2v{(2 * j < R && k < K) ? cv[2 * j] : 0.0f,
                    (2 * j + 1 < R && k < K) ? cv[2 * j + 1] : 0.0f} * splat2(own_scale);
 #pragma unroll
-    for (int j = 0; j < RP / 2; ++j)
-      accp[j] = from_pl ? f2v{2 * j < R ? Pl[((size_t)u * R + 2 * j) * 64 + lane] : 0.0f,
-                              2 * j + 1 < R ? Pl[((size_t)u * R + 2 * j + 1) * 64 + lane] : 0.0f}
-                        : splat2(0.0f);
-    walk_groups<RP, E, KIND, LOG, PFC>(src, lo, 64, jb, je, js, buf, own, Sl, El, lk, accp,
-                                       cnll);
+    for (int j = 0; j < RP / 2; ++j) accp[j] = splat2(0.0f);
+    walk_groups<RP, E, KIND, LOG>(src, lo, 64, jb, je, js, buf, own, Sl, El, lk, accp, cnll);
   };
   auto to_pl = [&](const f2v (&accp)[RP / 2]) {
 #pragma unroll
@@ -1997,25 +1893,10 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   };
 
   // 2. S-step over the wave's slices (next slice's reads in flight; the two register sets
-  //    alternate, as in spass_kernel); phase A after the first round when split
+  //    alternate, as in spass_kernel)
   if (il < nsl) {
     SliceIn<RP, E, ADAM> nxt;
-    bool more = one_slice(cur, nxt);  // round 1
-    if (split) {
-      __syncthreads();  // the first round's rows are in LDS
-      STAMP(wg, 15);
-      if (u < U) {
-        unit_begin(u, 1);
-        f2v accp[RP / 2];
-        unit_walk.template operator()<false>(false, accp);  // (the plain walk: registers)
-        to_pl(accp);
-        // the lane's NLL pair waits in this tile's dC slab rows (written only at the end of
-        // the launch, after phase B has read it back): no registers held across the rounds
-        reinterpret_cast<f2v*>(slab + (int64_t)t * R * Kp)[u * 64 + lane] = cnll;
-        cnll = splat2(0.0f);
-      }
-      STAMP(wg, 16);
-    }
+    const bool more = one_slice(cur, nxt);  // round 1 (peeled: its first-slice wait, n == 0)
     if (more)
       for (;;) {
         if (!one_slice(nxt, cur)) break;
@@ -2028,15 +1909,12 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
   if (t == 0 && tidx == 0) adam_cache_store(acache, ad, step_s + 2);
 
   STAMP(wg, 2);
-  if (u < U) {
-    unit_begin(u, split ? 2 : 0);
-    if (split) cnll = reinterpret_cast<const f2v*>(slab + (int64_t)t * R * Kp)[u * 64 + lane];
-  }
+  if (u < U) unit_begin(u);
   __syncthreads();  // the whole S tile is in LDS
   STAMP(wg, 3);
   for (; u < U; u += NW) {
     f2v accp[RP / 2];
-    unit_walk(split, accp);
+    unit_walk(accp);
     const float nll_w = wave_sum_dpp(cnll.x + cnll.y) * kLn2;
     cnll = splat2(0.0f);
     if (NP == 1) {
@@ -2050,7 +1928,7 @@ __device__ __forceinline__ void scfused_tile(QSC_SCF_PARAMS, const int t, const 
       to_pl(accp);
       if (lane == 0) Nl[u] = nll_w;
     }
-    if (u + NW < U) unit_begin(u + NW, 0);
+    if (u + NW < U) unit_begin(u + NW);
   }
   STAMP(wg, 4);
   if (NP > 1) {
@@ -2926,20 +2804,10 @@ static unsigned scpass_threads(const qsc_obs_desc* d, int R) {
   return 64u * (unsigned)std::min(rp_of(R) > 8 ? 8 : QSC_FUSED_WAVES, std::max(4, per));
 }
 
-QSC_API int32_t qsc_scpass_split_rows(const qsc_obs_desc* d, int32_t R) {
-  if (!QSC_PHASE_SPLIT || !desc_ok(d) || R < 1 || R > QSC_MAX_R) return 0;
-  const int NW = (int)(scpass_threads(d, R) / 64), nsl = d->PT / QSC_SLICE;
-  const int NP = cpass_parts(d, R, d->rowfmt == 1);
-  // the split needs part sums in LDS (NP > 1), one C-pass unit per wave and room for the
-  // phase-A NLL pairs in the tile's slab rows (2 NP <= R)
-  if (nsl < 2 * NW || NP < 2 || d->nks * NP > NW || 2 * NP > R) return 0;
-  return NW * QSC_SLICE;
-}
-
 QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32_t* s_width,
                        const int64_t* s_off, const void* c_entries, const int32_t* c_width,
-                       const int64_t* c_off, const int32_t* c_kmap, const int32_t* c_split,
-                       int32_t split_rows, const qsc_model* m, int32_t R, float* S,
+                       const int64_t* c_off, const int32_t* c_kmap, const qsc_model* m,
+                       int32_t R, float* S,
                        const float* C, float* mS, float* vS, const qsc_adam* adam,
                        float lambda_s, qsc_state* st, void* ws, size_t ws_bytes, void* stream) {
   if (!qsc_scpass_supported(d, R) || !m || m->nbounds - 1 != d->nbins || !S || !C || !mS ||
@@ -2965,9 +2833,6 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
   const qsc_adam ad = *adam;
   const unsigned threads = scpass_threads(d, R);
   (void)RP;
-  // the phase split applies only to lists split for exactly this launch's first S-step round
-  const int* split = (c_split && split_rows > 0 && split_rows == qsc_scpass_split_rows(d, R))
-                         ? c_split : nullptr;
   hipStream_t s = STREAM(stream);
 #define SCPASS_LAUNCH(RPV, ET, KD, LG)                                                         \
   do {                                                                                         \
@@ -2975,7 +2840,7 @@ QSC_API int qsc_scpass(const qsc_obs_desc* d, const void* s_entries, const int32
                          dim3(threads), shm, s, (const ET*)s_entries, s_width, s_off,         \
                          (const ET*)c_entries, c_width, c_off, c_kmap, d->nks, NP, d->PT, lk, E, \
                          d->nbins, R, d->K, S, C, mS, vS, ad, lambda_s, st, w.snll, w.snsq,    \
-                         w.slab, w.cnll, w.cnsq, w.acache, split);                             \
+                         w.slab, w.cnll, w.cnsq, w.acache);                                    \
   } while (0)
   QSC_DISPATCH_PASS(SCPASS_LAUNCH);
 #undef SCPASS_LAUNCH

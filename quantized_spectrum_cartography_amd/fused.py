@@ -27,7 +27,6 @@ class PassEngine:
         self.obs, self.R = obs, R
         # the packed entries at this rank (signed rows, or a code-field copy: obs.layout)
         self.desc, self.s_entries, self.c_entries = obs.layout(R)
-        self.split_rows = int(_lib.lib().qsc_scpass_split_rows(self.desc, R))
         dev = obs.device
         nb = _lib.lib().qsc_pass_workspace_bytes(self.desc, R)
         if nb == 0:
@@ -115,15 +114,12 @@ class PassEngine:
         return bool(_lib.lib().qsc_scpass_supported(self.desc, self.R))
 
     def scpass(self, S_pos, C, mS, vS, adam, lambda_s):
-        """spass (mode 1, Adam) fused with the next cpass at the updated S (qsc_scpass); with
-        the phase split of the lists when it was computed for this rank's launch."""
+        """spass (mode 1, Adam) fused with the next cpass at the updated S (qsc_scpass)."""
         self.gen += 1
         o = self.obs
-        split = o.split_rows and o.split_rows == self.split_rows
         _lib.call("qsc_scpass", self.desc, _lib.ptr(self.s_entries), _lib.ptr(o.s_width),
                   _lib.ptr(o.s_off), _lib.ptr(self.c_entries), _lib.ptr(o.c_width),
-                  _lib.ptr(o.c_off), _lib.ptr(o.c_kmap), _lib.ptr(o.c_split if split else None),
-                  int(o.split_rows if split else 0), o.model, self.R, _lib.ptr(S_pos),
+                  _lib.ptr(o.c_off), _lib.ptr(o.c_kmap), o.model, self.R, _lib.ptr(S_pos),
                   _lib.ptr(C), _lib.ptr(mS),
                   _lib.ptr(vS), adam, float(lambda_s), _lib.ptr(self.state), _lib.ptr(self.ws),
                   self.ws.numel(), _lib.stream())

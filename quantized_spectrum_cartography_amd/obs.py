@@ -144,13 +144,7 @@ class Observations:
         self.s_entries = torch.empty(desc.s_entries, dtype=et, device=dev)
         self.c_entries = torch.empty(desc.c_entries, dtype=et, device=dev)
         rowfmt = 1 if self.signed_rows_ok(R_hint) else 0
-        # the fused launch's phase split at R_hint (qsc_scpass_split_rows; 0 = none, or
-        # QSC_SPLIT=0); engines at another rank run unsplit
-        self.c_split = torch.zeros(nt * nks, dtype=torch.int32, device=dev)
         desc.rowfmt = rowfmt
-        self.split_rows = 0
-        if os.environ.get("QSC_SPLIT", "1") != "0":
-            self.split_rows = int(_lib.lib().qsc_scpass_split_rows(desc, int(R_hint)))
         # signed-row entries (include/qsc.h rowfmt 1: the one-bit kind reads each entry's code
         # through the gathered row) wherever the passes' doubled tables fit at this rank
         self._fill(rowfmt)
@@ -168,19 +162,12 @@ class Observations:
                   _lib.ptr(self.s_width), _lib.ptr(self.s_off), _lib.ptr(self.c_width),
                   _lib.ptr(self.c_off), _lib.ptr(self.c_kmap), _lib.ptr(s_entries),
                   _lib.ptr(c_entries), _lib.stream())
-        # phase split of the C-format lists for the fused launch at R_hint (qsc_obs_split; the
-        # same split for both entry formats: it depends only on the tile rows)
-        if self.split_rows:
-            _lib.call("qsc_obs_split", desc, _lib.ptr(self.c_width), _lib.ptr(self.c_off),
-                      _lib.ptr(c_entries), self.split_rows, _lib.ptr(self.c_split),
-                      _lib.stream())
         if self.schedule:
             # bank-conflict-free list order (include/qsc.h qsc_obs_schedule): the same order for
             # both entry formats (it depends only on the row residues), so their results agree
             ws = _ws(_lib.lib().qsc_obs_schedule_workspace_bytes(desc), self.device)
             _lib.call("qsc_obs_schedule", desc, _lib.ptr(self.s_width), _lib.ptr(self.s_off),
-                      _lib.ptr(self.c_width), _lib.ptr(self.c_off),
-                      _lib.ptr(self.c_split if self.split_rows else None), _lib.ptr(s_entries),
+                      _lib.ptr(self.c_width), _lib.ptr(self.c_off), _lib.ptr(s_entries),
                       _lib.ptr(c_entries), _lib.ptr(ws), ws.numel(), _lib.stream())
 
     def signed_rows_ok(self, R):

@@ -198,9 +198,19 @@ def graph_for(solver, n):
     if getattr(solver, "graph_capturable", True) is False:
         return None  # eager (the reason is in solver.graph_error)
     key = (n, solver.ahead()) if hasattr(solver, "ahead") else n
+    # a graph holds its tensors' addresses: a solver whose state tensors were swapped for others
+    # (sol.C = ...) captures anew instead of replaying into the old storage
+    ptrs = tuple(t.data_ptr() for t in (getattr(solver, a, None) for a in _STATE_TENSORS)
+                 if isinstance(t, torch.Tensor))
+    if solver.__dict__.get("_graph_ptrs") != ptrs:
+        graphs.clear()
+        solver._graph_ptrs = ptrs
     if key not in graphs:
         graphs[key] = _capture(solver, n, getattr(solver, "graph_tolerant", False))
     return graphs[key]
+
+
+_STATE_TENSORS = ("S", "C", "mS", "vS", "mC", "vC", "S_buf", "dS_buf", "dS_own", "red")
 
 
 def graph_chunks(n):

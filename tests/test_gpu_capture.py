@@ -82,14 +82,47 @@ def test_prepare_captures_every_chunk(monkeypatch):
     d = _random_case(73, 4, 64, 64, 64)
     sol = _solver(d)
     sol.prepare(10)
-    # chunks 4, 4, 2: the first starts with no C-pass ahead, the later ones with the C-pass the
-    # previous chunk's last fused launch left ahead (qmc.issue_iterations)
-    assert sorted(sol._graphs) == [(2, True), (4, False), (4, True)]
+    # chunks 4, 4, 2, each captured in both entry forms: without a C-pass ahead (a first run)
+    # and with the C-pass the previous chunk's or run's last fused launch left ahead
+    # (qmc.issue_iterations) -- so neither this run(10) nor a later one captures
+    assert sorted(sol._graphs) == [(2, False), (2, True), (4, False), (4, True)]
     calls = []
     orig = qmc._capture
     monkeypatch.setattr(qmc, "_capture", lambda *a: calls.append(a) or orig(*a))
     sol.run(10, use_graph=True)
+    sol.run(10, use_graph=True)
     assert calls == []
     ref = _solver(d)
     ref.run(10, use_graph=False)
+    ref.run(10, use_graph=False)
     assert np.array_equal(ref.S.cpu().numpy(), sol.S.cpu().numpy())
+
+
+def test_chained_run_redoes_a_c_pass_overwritten_in_between():
+    """a run that chains on the C-pass the previous run left ahead must not
+    use it when anything overwrote the workspace since -- here a direct engine C-pass at another
+    S (as bench.time_kernel or a tool would issue), which leaves S and C and their torch version
+    counters untouched.  The next run redoes its C-pass: the result equals an uninterrupted
+    run bit for bit."""
+    d = _random_case(74, 4, 64, 64, 64)
+    a = _solver(d)
+    a.run(3, use_graph=True)
+    assert a.ahead()
+    S_other = a.S * 2.0
+    a.engine.cpass(S_other, a.C)  # overwrites the slab partials the chain would use
+    assert not a.ahead()
+    a.run(3, use_graph=True)
+    ref = _solver(d)
+    ref.run(6, use_graph=False)
+    assert np.array_equal(ref.S.cpu().numpy(), a.S.cpu().numpy())
+    assert np.array_equal(ref.C.cpu().numpy(), a.C.cpu().numpy())
+    # a fresh tensor swapped in for C (version counter 0 again) also breaks the chain
+    b = _solver(d)
+    b.run(3, use_graph=True)
+    b.C = b.C.clone()
+    assert not b.ahead()
+    # and its next graph run captures anew at the new tensor (not a replay into the old one)
+    b.run(2, use_graph=True)
+    ref2 = _solver(d)
+    ref2.run(5, use_graph=False)
+    assert np.array_equal(ref2.C.cpu().numpy(), b.C.cpu().numpy())

@@ -158,7 +158,7 @@ def test_solver_graph_replay_matches_eager():
                           # one C-pass unit per tile (C2 shape class: K = 64, 128-position tiles)
                           (52, 4, 64, 64, 64, False, "probit", 2, 128),
                           (53, 4, 96, 64, 64, False, "probit", 2, None),
-                          # C3 shape class at 1024-position tiles: the phase-split fused launch
+                          # C3 shape class at 1024-position tiles
                           (55, 8, 128, 128, 256, False, "probit", 2, 1024)])
 def test_fused_spass_cpass_bitexact(seed, R, I, J, K, log_model, loss, nbins, tile):
     """qsc_scpass (S-step + next C-pass in one launch) reproduces spass + cpass bit for bit:
@@ -419,8 +419,14 @@ def test_dip_solver_256_vs_oracle_graph():
 @pytest.mark.parametrize("optimize", ["z", "weights"])
 def test_generator_solver_graph_equals_eager(optimize):
     """GeneratorSolver: the captured-hipGraph run (chunk graphs after one eager iteration) and
-    the eager op sequence give the same S, C, Z and costs bit for bit (same kernels on the same
-    buffers), at C5's size with the 256^2 decoder."""
+    the eager op sequence give the same S, C, Z and costs at C5's size with the 256^2 decoder.
+    Not bit for bit: MIOpen picks its convolution algorithms per call site and workspace (the
+    capture allocates from the graph's pool), and those differ in rounding -- measured ~1e-6
+    relative after 7 iterations (round 6); the HIP passes themselves replay bit for bit
+    (test_solver_graph_replay_matches_eager).  z: Adam on Z, 7 iterations (two chunk graphs),
+    1e-5.  weights: Adam on the decoder weights, whose sign steps amplify rounding chaotically
+    (1.6e-3 apart after 7 iterations; test_dip_solver_vs_oracle's reason), so 2 iterations (one
+    graph step after the eager one) at that test's 5e-4."""
     import copy
     from quantized_spectrum_cartography_amd import dip, qmc
     dec, Z0, C0, Y, Wx, b, off = _dip256_case(seed=4)
@@ -430,17 +436,18 @@ def test_generator_solver_graph_equals_eager(optimize):
         out = []
         for g in (False, True):
             r = dip.solve(Y, Wx, b, 5.0, 4, offset=off, decoder=copy.deepcopy(dec).cuda(),
-                          Z_init=Z0, C_init=C0, max_iter=7, lr_s=1e-3, optimize=optimize,
-                          use_graph=g)
+                          Z_init=Z0, C_init=C0, max_iter=7 if optimize == "z" else 2,
+                          lr_s=1e-3, optimize=optimize, use_graph=g)
             out.append(r)
     finally:
         qmc.GEN_GRAPH_ITERS = old
     a, c = out
-    assert c.graph_error is None and len(c.solver._graphs) == 2
-    assert np.array_equal(a.S.cpu().numpy(), c.S.cpu().numpy())
-    assert np.array_equal(a.C.cpu().numpy(), c.C.cpu().numpy())
-    assert np.array_equal(a.Z.cpu().numpy(), c.Z.cpu().numpy())
-    assert a.costs_c == c.costs_c and a.costs_s == c.costs_s
+    assert c.graph_error is None and len(c.solver._graphs) == (2 if optimize == "z" else 1)
+    tol = 1e-5 if optimize == "z" else 5e-4
+    assert rel_fro(a.S.cpu().numpy(), c.S.cpu().numpy()) < tol
+    assert rel_fro(a.C.cpu().numpy(), c.C.cpu().numpy()) < tol
+    assert rel_fro(a.Z.cpu().numpy(), c.Z.cpu().numpy()) < tol
+    assert np.allclose(a.costs_c, c.costs_c, rtol=tol) and np.allclose(a.costs_s, c.costs_s, rtol=tol)
 
 
 def test_dip_solver_256():
@@ -758,32 +765,6 @@ def test_chained_runs_equal_one_run_and_the_unchained_form(use_graph):
     parts.run(2, use_graph=use_graph)
     plain.run(2, use_graph=use_graph)
     assert torch.equal(parts.S, plain.S) and torch.equal(parts.C, plain.C)
-
-
-def test_phase_split_fused_launch_is_bitexact():
-    """The phase-split fused launch (C-pass chunks j < c_split walked right after the first
-    S-step round, include/qsc.h qsc_scpass) gives the unsplit launch's S, C and costs bit for
-    bit, and the split really applies at the C3 shape class."""
-    from quantized_spectrum_cartography_amd import qmc
-    from quantized_spectrum_cartography_amd.obs import Observations
-    d = _random_case(56, 8, 128, 128, 256)
-    o = Observations(d["Y"], d["Wx"], d["b"], d["sigma"], R_hint=8, tile=1024)
-    if o.split_rows == 0:
-        pytest.skip("library built without the phase split (QSC_PHASE_SPLIT=0, the default)")
-    assert o.split_rows == 16 * 32 and int(o.c_split.min()) > 0
-    kw = dict(S_init=d["S0"], C_init=d["C0"], max_iter=9)
-    a = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], obs=o, **kw)
-    # the same lists launched without the split (engines pass c_split only when the layout's
-    # split_rows matches their launch)
-    rows, o.split_rows = o.split_rows, 0
-    try:
-        b = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], obs=o, **kw)
-    finally:
-        o.split_rows = rows
-    assert a.fused and b.fused
-    assert np.array_equal(a.S.cpu().numpy(), b.S.cpu().numpy())
-    assert np.array_equal(a.C.cpu().numpy(), b.C.cpu().numpy())
-    assert a.costs_c == b.costs_c and a.costs_s == b.costs_s
 
 
 @pytest.mark.parametrize("log_model,R,I,J,K,s_scale,lr_s,n", [
