@@ -440,7 +440,7 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
           betas=(0.9, 0.999), eps=1e-8, project_c=True, generator=None, Z_init=None,
           restart=False, restart_samples=(200, 200), T_true=None, nmse_every=0,
           use_graph=False, obs=None, tile=None, callback=None, loss="probit", fuse=True,
-          project_s=None):
+          project_s=None, holdout=0.0, check_every=10, patience=5, holdout_seed=0):
     """Alternating S/C probit-MLE (qmc/qmc.ipynb :559-645).
 
     Args mirror the notebook globals: Y (K,1,I,J) bin indices, Wx (K,1,I,J) 0/1 mask,
@@ -455,6 +455,13 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
     qmc/quantization_model_log.py:14, qmc/qmc.ipynb:571), which unprojected free S leaves within
     a few hundred steps, and the reference's own S is a sigmoid output (>= 0); False otherwise.
     project_s=False under the log model is accepted (the caller's choice) and warns.
+    holdout > 0 (free S only; not in the reference, which runs a fixed iteration count): that
+    fraction of the observed entries (seeded by holdout_seed) is held out of the fit; every
+    `check_every` iterations their NLL at the current S, C is evaluated (fused HIP S-pass on
+    the held-out set, same pixel order), and the run stops once it has not improved for
+    `patience` checks, returning the S, C of the best check (result.best_iter, .holdout_nll).
+    With ~6 one-bit samples per pixel (C2) the unregularised free-S MLE over-fits: the map
+    NMSE is best after ~50 iterations and grows after.
     Returns a SolveResult with S (R,1,I,J) and C (R,K) on the GPU.
     """
     if log_model and obs is None:
@@ -467,11 +474,27 @@ def solve(Y, Wx, bin_boundaries, noise_std, R=None, S_init=None, C_init=None, of
     if R is None:
         R = (S_init.shape[0] if S_init is not None else
              (C_init.shape[0] if C_init is not None else Z_init.shape[0]))
+    obs_h = None
+    if holdout and generator is None:
+        if obs is not None:
+            raise ValueError("holdout splits the observations itself: pass Y, Wx, not obs")
+        Wx_fit, Wx_h = split_holdout(Y, Wx, float(holdout), holdout_seed)
+        obs = Observations(Y, Wx_fit, bin_boundaries, noise_std, offset=offset or 0.0,
+                           log_model=log_model, tile=tile, R_hint=R, loss=loss)
+        # the held-out entries in the SAME position order (perm) and tiles, so the solver's
+        # position-order S is evaluated on them as it is
+        obs_h = Observations(Y, Wx_h, bin_boundaries, noise_std, offset=offset or 0.0,
+                             log_model=log_model, tile=obs.desc.PT, R_hint=R, loss=loss,
+                             perm=obs.perm)
     if obs is None:
         obs = Observations(Y, Wx, bin_boundaries, noise_std, offset=offset or 0.0,
                            log_model=log_model, tile=tile, R_hint=R, loss=loss)
     if C_init is None:
         C_init = torch.zeros(R, K)
+    if generator is None and obs_h is not None:
+        return _solve_holdout(obs, obs_h, S_init, C_init, R, lambda_c, lambda_s, lr_c, lr_s,
+                              max_iter, betas, eps, project_c, fuse, project_s, use_graph,
+                              int(check_every), int(patience))
     if generator is None:
         if S_init is None:
             S_init = torch.zeros(R, 1, I, J)
@@ -686,6 +709,51 @@ def _gen_chunks(n):
         out.append(m)
         n -= m
     return out
+
+
+def split_holdout(Y, Wx, frac, seed=0):
+    """(Wx_fit, Wx_holdout): a seeded random `frac` of the observed entries (Wx == 1, or all
+    entries when Wx is None) moved to the held-out mask."""
+    W = (Wx if Wx is not None else torch.ones(Y.shape)).to(torch.float32)
+    g = torch.Generator().manual_seed(int(seed))
+    u = torch.rand(W.shape, generator=g).to(W.device)
+    hold = (W > 0) & (u < frac)
+    return W * (~hold).to(W.dtype), W * hold.to(W.dtype)
+
+
+def _solve_holdout(obs, obs_h, S_init, C_init, R, lambda_c, lambda_s, lr_c, lr_s, max_iter,
+                   betas, eps, project_c, fuse, project_s, use_graph, check_every, patience):
+    """Free-S solve with early stopping on the held-out NLL (solve(holdout=...))."""
+    I, J = obs.I, obs.J
+    if S_init is None:
+        S_init = torch.zeros(R, 1, I, J)
+    sol = FreeSSolver(obs, S_init, C_init, lambda_c, lambda_s, lr_c, lr_s, betas, eps, project_c,
+                      hist_cap=max_iter, fuse=fuse, project_s=project_s)
+    eng_h = PassEngine(obs_h, R)
+    eng_h.init_state(sol.S)
+    dS_h = torch.empty_like(sol.S)
+    hist_h, best, best_iter, best_SC = [], float("inf"), 0, None
+    done = 0
+    while done < max_iter:
+        n = min(check_every, max_iter - done)
+        sol.run(n, use_graph=use_graph)
+        done += n
+        eng_h.spass(sol.S, sol.C, 0, dS=dS_h)
+        eng_h.flush(record=False)
+        v = float(eng_h.read_state()["nll_s"])
+        hist_h.append((done, v))
+        if v < best:
+            best, best_iter = v, done
+            best_SC = (sol.S.clone(), sol.C.clone())
+        elif done - best_iter >= patience * check_every:
+            break
+    costs_c, costs_s = sol.history()
+    S_pos, C = best_SC if best_SC is not None else (sol.S, sol.C)
+    res = SolveResult(S=obs.to_pixels(S_pos, R).reshape(R, 1, I, J), C=C.clone(),
+                      costs_c=costs_c, costs_s=costs_s, iters=done, fused=sol.fuse)
+    res.best_iter = best_iter
+    res.holdout_nll = hist_h
+    return res
 
 
 def _solve_generator(obs, generator, Z_init, C_init, R, lambda_c, lambda_s, lr_c, lr_s, max_iter,

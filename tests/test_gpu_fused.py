@@ -424,9 +424,11 @@ def test_generator_solver_graph_equals_eager(optimize):
     capture allocates from the graph's pool), and those differ in rounding -- measured ~1e-6
     relative after 7 iterations (round 6); the HIP passes themselves replay bit for bit
     (test_solver_graph_replay_matches_eager).  z: Adam on Z, 7 iterations (two chunk graphs),
-    1e-5.  weights: Adam on the decoder weights, whose sign steps amplify rounding chaotically
-    (1.6e-3 apart after 7 iterations; test_dip_solver_vs_oracle's reason), so 2 iterations (one
-    graph step after the eager one) at that test's 5e-4."""
+    1e-5.  weights: Adam on the decoder weights: MIOpen's backward-weights convolutions are not
+    bitwise reproducible run to run, and Adam's first steps are sign steps that turn those
+    rounding differences into +-lr moves of the near-zero-gradient weights
+    (test_dip_solver_vs_oracle's reason): 1.6e-3 apart after 7 iterations, 1.0e-3 after 2 (the
+    returned S is the forward at the weights after ONE step), so 2 iterations at 5e-3."""
     import copy
     from quantized_spectrum_cartography_amd import dip, qmc
     dec, Z0, C0, Y, Wx, b, off = _dip256_case(seed=4)
@@ -443,7 +445,7 @@ def test_generator_solver_graph_equals_eager(optimize):
         qmc.GEN_GRAPH_ITERS = old
     a, c = out
     assert c.graph_error is None and len(c.solver._graphs) == (2 if optimize == "z" else 1)
-    tol = 1e-5 if optimize == "z" else 5e-4
+    tol = 1e-5 if optimize == "z" else 5e-3
     assert rel_fro(a.S.cpu().numpy(), c.S.cpu().numpy()) < tol
     assert rel_fro(a.C.cpu().numpy(), c.C.cpu().numpy()) < tol
     assert rel_fro(a.Z.cpu().numpy(), c.Z.cpu().numpy()) < tol
@@ -781,7 +783,7 @@ def test_project_s_matches_reference_op_sequence(log_model, R, I, J, K, s_scale,
         s_scale * torch.rand(R, 1, I, J, generator=torch.Generator().manual_seed(5))
     kw = dict(offset=d["offset"], log_model=log_model, lr_s=lr_s)
     free = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], S_init=S0, C_init=d["C0"],
-                     max_iter=n, **kw)
+                     max_iter=n, project_s=False, **kw)  # (the log model's default projects)
     assert bool((free.S < 0).any()), "the case must drive some of S below 0"
     res = qmc.solve(d["Y"], d["Wx"], d["b"], d["sigma"], S_init=S0, C_init=d["C0"],
                     max_iter=n, project_s=True, **kw)

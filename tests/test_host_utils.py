@@ -105,3 +105,21 @@ def test_fused_finish_ticket_protocol():
                 # the waiters' count is reached exactly at the launch's last arrival
                 assert done_at == nt - 1
                 assert ctr["groups"] == (start_launch + launch + 1) * G
+
+
+def test_split_holdout_partitions_the_observed_entries():
+    """qmc.split_holdout: the fit and held-out masks partition the observed entries, the
+    held-out share is about `frac`, and the split is a function of the seed."""
+    import torch
+    from quantized_spectrum_cartography_amd.qmc import split_holdout
+    g = torch.Generator().manual_seed(3)
+    Y = torch.zeros(16, 1, 20, 20, dtype=torch.int64)
+    Wx = torch.bernoulli(torch.full((16, 1, 20, 20), 0.3), generator=g)
+    a, b = split_holdout(Y, Wx, 0.1, seed=7)
+    assert torch.equal(a + b, Wx) and torch.all(a * b == 0)
+    frac = float(b.sum() / Wx.sum())
+    assert 0.07 < frac < 0.13
+    a2, b2 = split_holdout(Y, Wx, 0.1, seed=7)
+    assert torch.equal(b, b2)
+    _, b3 = split_holdout(Y, None, 0.1, seed=7)
+    assert float(b3.mean()) > 0.07

@@ -12,10 +12,11 @@ stop() { echo "STOP rc=$1 at $2"; exit $1; }
 faulted() { grep -qE "illegal memory access|Memory access fault|hipErrorIllegalAddress|HSA_STATUS_ERROR|GPU core dump" "$1"; }
 cd $R
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $G/pytest_gpu.log 2>&1; rc=$?
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $G/pytest_gpu.log 2>&1; rc=$?
   tail -4 $G/pytest_gpu.log
   faulted $G/pytest_gpu.log && stop 99 pytest-fault
-  [ $rc -ne 0 ] && stop $rc pytest
+  [ $rc -ge 124 ] && stop $rc pytest-timeout
+  grep -E "^(FAILED|ERROR)" $G/pytest_gpu.log | head -10
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $G/smoke.log 2>&1 || stop $? smoke
   tail -2 $G/smoke.log
 fi

@@ -9,6 +9,8 @@ Prints one JSON line of trajectories (map NMSE every few iterations, qmc/quantiz
               fused launches, the bench's workload at C2 size; map NMSE at log-spaced iterations
               and the best along the path (free S at ~6 one-bit samples per pixel over-fits);
   c2_free_s_f05  the same map sampled at f = 0.5 (onebit_lowrank.ipynb's f).
+  c2_*_holdout_stop  the same runs stopped on the NLL of 10 % held-out observations
+              (qmc.solve(holdout=0.1)): the stopping rule, without T_true.
   c5_*        a generate_map-style radio map (maps.generate_map: Gaussian PSD bumps, path loss x
               FFT-correlated log-normal shadowing, 256 x 256, K = 64, R = 4) quantized with the log
               model as qmc/qmc.ipynb :537 does (4 log bins, LOG_OFFSET_4, sigma = 5), f = 0.1:
@@ -80,7 +82,21 @@ def main():
                      "slf_nmse": metrics.slf_nmse(res.S, p["S_true"]),
                      "cost_first": res.costs_s[0], "cost_last": res.costs_s[-1]}
         print(json.dumps({name: [tr[-1], best]}), file=sys.stderr, flush=True)
-        del p, res
+        # the same run stopped on 10 % held-out observations (qmc.solve(holdout=...)): no
+        # knowledge of T_true, the stopping rule the free-S MLE needs at these sample counts
+        t0 = time.perf_counter()
+        es = qmc.solve(p["Y"], p["Wx"], p["b"], p["sigma"], S_init=p["S0"], C_init=p["C0"],
+                       max_iter=args.c2_iters, use_graph=True, holdout=0.1, check_every=10,
+                       patience=5)
+        torch.cuda.synchronize()
+        out[name + "_holdout_stop"] = {
+            "holdout": 0.1, "check_every": 10, "patience": 5, "stopped_at": es.iters,
+            "best_iter": es.best_iter, "wall_s": time.perf_counter() - t0,
+            "map_nmse": float(metrics.map_nmse(es.S, es.C, p["T_true"])),
+            "slf_nmse": metrics.slf_nmse(es.S, p["S_true"])}
+        print(json.dumps({name + "_holdout_stop": out[name + "_holdout_stop"]}), file=sys.stderr,
+              flush=True)
+        del p, res, es
 
     # ---- C5: generated map, log model ----
     K, R, N = 64, 4, 256
