@@ -408,6 +408,13 @@ QSC_API int qsc_cpass_nsq(const qsc_obs_desc* d, const void* c_entries, const in
 QSC_API int64_t qsc_pass_cnsq_offset(const qsc_obs_desc* d, int32_t R);
 /* ||x||^2 into *out (fp32, fixed order), e.g. the local ||C_slab||^2 before an all-reduce */
 QSC_API int qsc_sumsq_small(const float* x, int32_t n, float* out, void* stream);
+/* Adam (torch.optim.Adam's update, bit for bit with torch 2.x's single-tensor CPU path) on a flat
+ * buffer of n parameters p with moments m, v and gradient g, at step = st->iter: the S-pass
+ * counter, i.e. the S-step this update belongs to -- the generator / DIP solver's step on Z or
+ * the decoder weights (qmc/qmc.ipynb :634), which a captured hipGraph then replays for every
+ * iteration. */
+QSC_API int qsc_adam_flat(float* p, float* m, float* v, const float* g, int64_t n,
+                          const qsc_adam* adam, const qsc_state* st, void* stream);
 /* debug builds (QSC_DEBUG=1, _build.py --debug): the source line of the last failed bounds
  * check in the pass kernels (entry offsets, gather-table rows, lane bins; a failed check is
  * recorded and its index clamped, never trapped), 0 if none, -1 in release builds.

@@ -2409,6 +2409,29 @@ __global__ void __launch_bounds__(1024) sumsq_small_kernel(const float* __restri
   if (threadIdx.x == 0) *out = r;
 }
 
+// Adam on a flat parameter buffer (the generator / DIP solver's decoder weights or latent Z,
+// torch.optim.Adam's update bit for bit: adam_elem) at step = the state's S-pass counter, so one
+// captured hipGraph replays every iteration's step (qsc_adam_flat)
+__global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p,
+                                                        float* __restrict__ m,
+                                                        float* __restrict__ v,
+                                                        const float* __restrict__ g, int64_t n,
+                                                        qsc_adam ad,
+                                                        const qsc_state* __restrict__ st) {
+  __shared__ AdamScalars sc;
+  if (threadIdx.x == 0) sc = adam_scalars(ad, st->iter);
+  __syncthreads();
+  const AdamScalars s = sc;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float pp = p[i], mm = m[i], vv = v[i];
+    adam_elem(pp, mm, vv, g[i], ad, s);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+  }
+}
+
 __global__ void selftest_erf_kernel(const float* __restrict__ x, int n, float* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -2951,6 +2974,17 @@ QSC_API int qsc_slice_nsq(const qsc_obs_desc* d, int32_t R, const float* S, void
     hipLaunchKernelGGL(slice_nsq_kernel<8>, grid, blk, 0, hs, nslices, S, w.snsq);
   else
     hipLaunchKernelGGL(slice_nsq_kernel<16>, grid, blk, 0, hs, nslices, S, w.snsq);
+  QSC_CHECK_LAUNCH();
+  return QSC_OK;
+}
+
+QSC_API int qsc_adam_flat(float* p, float* m, float* v, const float* g, int64_t n,
+                          const qsc_adam* adam, const qsc_state* st, void* stream) {
+  if (n < 0 || !adam || !st || (n > 0 && (!p || !m || !v || !g))) return QSC_EINVAL;
+  if (n == 0) return QSC_OK;
+  const int64_t blocks = std::min<int64_t>(ceil_div(n, 256), (int64_t)cu_count() * 8);
+  hipLaunchKernelGGL(adam_flat_kernel, dim3((unsigned)blocks), dim3(256), 0, STREAM(stream), p,
+                     m, v, g, n, *adam, st);
   QSC_CHECK_LAUNCH();
   return QSC_OK;
 }

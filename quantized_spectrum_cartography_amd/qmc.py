@@ -543,11 +543,13 @@ class GeneratorSolver:
               the persistent S_pos), fused HIP S-pass in gradient mode (dS), qsc_state_flush
               (the S-step NLL into the history row), dS -> pixel order, the surrogate
               <S, dS> + lambda_s ||Z||_F back-propagated through the generator (:626-633), the
-              optimizer step (:634) -- torch Adam with capturable=True, so its step counters
-              live on the device; lambda_s ||Z|| recorded on the device.
+              optimizer step (:634) -- qsc_adam_flat over the flat parameter buffer, its step
+              the engine state's S-step count; lambda_s ||Z|| recorded on the device.
     run(n, use_graph=True) replays captured chunk graphs of GEN_GRAPH_ITERS iterations (sharing
-    one memory pool) after WARMUP eager iterations, which create the optimizer state and the
-    autograd / MIOpen workspaces outside capture.  Graph replay and eager issue run the same
+    one memory pool) after WARMUP eager iterations, which create the autograd / MIOpen
+    workspaces outside capture.  The optimised tensors live in one flat buffer and take their
+    Adam step in one launch (qsc_adam_flat: torch.optim.Adam's update bit for bit, the step
+    count from the engine state).  Graph replay and eager issue run the same
     kernels on the same buffers, so the results are bitwise equal
     (tests/test_gpu_fused.py::test_generator_solver_graph_equals_eager).  A capture that fails
     (a library call that cannot be captured) is recorded in `graph_error` and the solver runs
@@ -566,12 +568,34 @@ class GeneratorSolver:
         self.mC, self.vC = torch.zeros_like(self.C), torch.zeros_like(self.C)
         self.adam_c = _lib.make_adam(lr_c, betas, eps, project_nonneg=project_c)
         self.lambda_c, self.lambda_s = float(lambda_c), float(lambda_s)
-        self.Z = Z_init.detach().to(dev, torch.float32).clone().requires_grad_(bool(optimize_z))
-        self.plist = ([self.Z] if optimize_z else []) + list(params or [])
-        # capturable: the step counters are device tensors, so one captured optimizer step is
-        # valid at every replay (the eager iterations run the same capturable update)
-        self.optS = torch.optim.Adam(self.plist, lr=lr_s, betas=betas, eps=eps,
-                                     capturable=True)
+        # The optimised tensors (Z and / or the decoder's parameters) live in ONE flat buffer
+        # (each a view into it), so the S-step's Adam is one qsc_adam_flat launch over all of
+        # them -- torch.optim.Adam's update bit for bit, at the step the engine state counts --
+        # instead of torch's per-tensor launches (its capturable foreach path divides every
+        # tensor by its 0-dim bias corrections in a launch of its own: ~150 launches of a few us
+        # per iteration for the 256^2 decoder, round 6's profile).
+        Z = Z_init.detach().to(dev, torch.float32)
+        plist = list(params or [])
+        sizes = ([Z.numel()] if optimize_z else []) + [q.numel() for q in plist]
+        self.flat = torch.empty(sum(sizes), dtype=torch.float32, device=dev)
+        o = 0
+        if optimize_z:
+            self.flat[:Z.numel()] = Z.reshape(-1)
+            self.Z = self.flat[:Z.numel()].view(Z.shape).detach().requires_grad_(True)
+            o = Z.numel()
+        else:
+            self.Z = Z.clone()
+        for q in plist:
+            n = q.numel()
+            with torch.no_grad():
+                self.flat[o:o + n] = q.detach().reshape(-1).to(dev, torch.float32)
+                q.data = self.flat[o:o + n].view(q.shape)
+            o += n
+        self.plist = ([self.Z] if optimize_z else []) + plist
+        self.m_flat = torch.zeros_like(self.flat)
+        self.v_flat = torch.zeros_like(self.flat)
+        self.g_flat = torch.zeros_like(self.flat)
+        self.adam_s = _lib.make_adam(lr_s, betas, eps, project_nonneg=False)
         with torch.no_grad():
             S0 = generator(self.Z).reshape(R, 1, self.I, self.J)
         self.S_pos = obs.to_positions(S0.reshape(R, -1))
@@ -597,7 +621,11 @@ class GeneratorSolver:
 
     def s_step(self):
         e, R = self.engine, self.R
-        self.optS.zero_grad(set_to_none=False)
+        # gradients set to None: backward then writes each one instead of zeroing and adding to
+        # it (two elementwise launches per parameter tensor); inside a capture the new gradients
+        # live in the graph's pool
+        for q in self.plist:
+            q.grad = None
         S = self.net(self.Z).reshape(R, 1, self.I, self.J)
         self.obs.to_positions(S.detach().reshape(R, -1), out=self.S_pos)
         e.spass(self.S_pos, self.C, 0, dS=self.dS_pos)
@@ -606,7 +634,12 @@ class GeneratorSolver:
         reg = self.lambda_s * torch.norm(self.Z, "fro")
         surrogate = (S * self.dS_pix.reshape(R, 1, self.I, self.J)).sum() + reg
         surrogate.backward()
-        self.optS.step()
+        if self.plist:
+            # the gradients into the flat buffer (one batched copy), then Adam on all of them
+            torch.cat([q.grad.reshape(-1) for q in self.plist], out=self.g_flat)
+            _lib.call("qsc_adam_flat", _lib.ptr(self.flat), _lib.ptr(self.m_flat),
+                      _lib.ptr(self.v_flat), _lib.ptr(self.g_flat), self.flat.numel(),
+                      self.adam_s, _lib.ptr(e.state), _lib.stream())
         with torch.no_grad():
             self.zreg.index_copy_(0, self.ctr.clamp(max=self.hist_cap - 1),
                                   reg.detach().reshape(1))
