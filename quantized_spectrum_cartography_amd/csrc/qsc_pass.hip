@@ -1366,6 +1366,9 @@ constexpr int kCTBlock = 1024;
 #ifndef QSC_CTILE_W16
 #define QSC_CTILE_W16 8
 #endif
+#ifndef QSC_CTILE_SREG
+#define QSC_CTILE_SREG 4
+#endif
 template <int RP>
 struct CTBlock {
   static constexpr int w = RP > 8 ? QSC_CTILE_W16 : kCTBlock / 64;  // max waves
@@ -1423,17 +1426,42 @@ __global__ void __launch_bounds__(CTBlock<RP>::v) cpass_tile_kernel(
 #pragma unroll
     for (int r = 0; r < RP; ++r) cv[r] = C[(int64_t)min(r, R - 1) * K + min(k, K - 1)];
   };
+  // the tile's S rows are read first, into registers when they fit QSC_CTILE_SREG float4 per
+  // thread: the unit's reads below wait on their own dependent reads (bounds -> entries, bin ->
+  // C column), so rows issued after them arrived one round trip later
+  const float4* __restrict__ src4 = reinterpret_cast<const float4*>(S);
+  constexpr int V = RP / 4;  // float4 per row
+  // (not for 32-bit entries below rank 16: their 16-wave walk has no VGPRs to spare)
+  constexpr bool kSRok = QSC_CTILE_SREG > 0 && (RP > 8 || sizeof(E) == 2);
+  constexpr int kSR = kSRok ? QSC_CTILE_SREG : 1;
+  const bool sreg = kSRok && PT * V <= kSR * (int)blockDim.x;
+  float4 srow[kSR];
+  if (sreg) {
+#pragma unroll
+    for (int q = 0; q < kSR; ++q) {
+      const int i = (int)threadIdx.x + q * (int)blockDim.x;
+      const int ql = i / V, c = i - ql * V;
+      if (i < PT * V) srow[q] = src4[tile_pos(t, ql, (int)gridDim.x) * V + c];
+    }
+  }
   if (u < U) unit_begin(u);
 
   // 2. stage the pixel tile (whole position slices, 16-B reads / writes at pitch SP)
   {
-    const float4* __restrict__ src4 = reinterpret_cast<const float4*>(S);
-    constexpr int V = RP / 4;  // float4 per row
     const int nt = gridDim.x;
+    if (sreg) {
+#pragma unroll
+      for (int q = 0; q < kSR; ++q) {
+        const int i = (int)threadIdx.x + q * (int)blockDim.x;
+        const int ql = i / V, c = i - ql * V;
+        if (i < PT * V) put_row4<RP, KIND>(Sl, PT, ql, 4 * c, srow[q], lk.ob_thr);
+      }
+    } else {
 #pragma unroll 4
-    for (int i = threadIdx.x; i < PT * V; i += blockDim.x) {
-      const int ql = i / V, c = i - ql * V;
-      put_row4<RP, KIND>(Sl, PT, ql, 4 * c, src4[tile_pos(t, ql, nt) * V + c], lk.ob_thr);
+      for (int i = threadIdx.x; i < PT * V; i += blockDim.x) {
+        const int ql = i / V, c = i - ql * V;
+        put_row4<RP, KIND>(Sl, PT, ql, 4 * c, src4[tile_pos(t, ql, nt) * V + c], lk.ob_thr);
+      }
     }
     put_pad_row<RP, KIND>(Sl, PT);
   }
