@@ -1369,6 +1369,9 @@ constexpr int kCTBlock = 1024;
 #ifndef QSC_CTILE_SREG
 #define QSC_CTILE_SREG 4
 #endif
+#ifndef QSC_CTILE_CT
+#define QSC_CTILE_CT 1
+#endif
 template <int RP>
 struct CTBlock {
   static constexpr int w = RP > 8 ? QSC_CTILE_W16 : kCTBlock / 64;  // max waves
@@ -1379,7 +1382,7 @@ template <int RP, typename E, int KIND, bool LOG>
 __global__ void __launch_bounds__(CTBlock<RP>::v) cpass_tile_kernel(
     const E* __restrict__ ent, const int* __restrict__ width, const int64_t* __restrict__ off,
     const int* __restrict__ kmap, int nks, int NP, int PT, Lik lk, Edges E_, int nbins, int R,
-    int K,
+    int K, int ct_in,
     const float* __restrict__ S, const float* __restrict__ C, float* __restrict__ slab,
     float* __restrict__ part_nll, float* __restrict__ cnsq, float* __restrict__ snsq_out) {
   using T = Ent<E>;
@@ -1395,6 +1398,10 @@ __global__ void __launch_bounds__(CTBlock<RP>::v) cpass_tile_kernel(
   (void)TR;
 
   float* Nl = Pl + (NP > 1 ? (size_t)U * R * 64 : 0);             // [U] / [NW]
+  // (ct) C^T staged next to the tile, [K][RP] (rows r >= R unread), for the units' C columns
+  // (not for 32-bit entries below rank 16: their 16-wave walk has no VGPRs to spare)
+  float* Ctl = Nl + ((max(U, 16) + 3) & ~3);
+  const bool ct = (RP > 8 || sizeof(E) == 2) && ct_in != 0;
   const int t = blockIdx.x;
   const int Kp = nks * 64;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1410,7 +1417,23 @@ __global__ void __launch_bounds__(CTBlock<RP>::v) cpass_tile_kernel(
   int wi = 0, j0 = 0, j1 = 0, js = 1, k = 0;
   const V4* src = nullptr;
   const uint32_t lo = (uint32_t)lane * (uint32_t)sizeof(V4);
-  auto unit_begin = [&](int uu) {
+  // the unit's C column: from the staged C^T (ct; after the staging barrier) or from C
+  auto unit_cols = [&]() {
+    if (ct) {
+#pragma unroll
+      for (int r = 0; r < RP; r += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(Ctl + (size_t)min(k, K - 1) * RP + r);
+        cv[r] = q.x;
+        cv[r + 1] = q.y;
+        cv[r + 2] = q.z;
+        cv[r + 3] = q.w;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < RP; ++r) cv[r] = C[(int64_t)min(r, R - 1) * K + min(k, K - 1)];
+    }
+  };
+  auto unit_begin = [&](int uu, bool cols) {
     const int ks = uu / NP, part = uu - ks * NP;
     wi = t * nks + ks;
     const int W4 = width[wi] >> 2;
@@ -1423,8 +1446,7 @@ __global__ void __launch_bounds__(CTBlock<RP>::v) cpass_tile_kernel(
     load_group(src, lo, 64, j0, js, max(j1 - 1, 0), buf);
     k = kmap[wi * 64 + lane];  // this lane's bin (count-sorted order)
     QSC_DCHECK(k >= 0 && k < Kp);
-#pragma unroll
-    for (int r = 0; r < RP; ++r) cv[r] = C[(int64_t)min(r, R - 1) * K + min(k, K - 1)];
+    if (cols) unit_cols();
   };
   // the tile's S rows are read first, into registers when they fit QSC_CTILE_SREG float4 per
   // thread: the unit's reads below wait on their own dependent reads (bounds -> entries, bin ->
@@ -1444,11 +1466,31 @@ __global__ void __launch_bounds__(CTBlock<RP>::v) cpass_tile_kernel(
       if (i < PT * V) srow[q] = src4[tile_pos(t, ql, (int)gridDim.x) * V + c];
     }
   }
-  if (u < U) unit_begin(u);
+  // (ct) the C^T reads: no dependency, so they ride with the S rows' round trip
+  constexpr int kCT = 4;  // C floats per thread held in registers (R K <= kCT * blockDim)
+  float ctv[kCT];
+  if (ct) {
+#pragma unroll
+    for (int q = 0; q < kCT; ++q) {
+      const int i = (int)threadIdx.x + q * (int)blockDim.x;
+      if (i < R * K) ctv[q] = C[i];
+    }
+  }
+  if (u < U) unit_begin(u, !ct);
 
   // 2. stage the pixel tile (whole position slices, 16-B reads / writes at pitch SP)
   {
     const int nt = gridDim.x;
+    if (ct) {
+#pragma unroll
+      for (int q = 0; q < kCT; ++q) {
+        const int i = (int)threadIdx.x + q * (int)blockDim.x;
+        if (i < R * K) {
+          const int r = i / K, kk = i - r * K;
+          Ctl[(size_t)kk * RP + r] = ctv[q];
+        }
+      }
+    }
     if (sreg) {
 #pragma unroll
       for (int q = 0; q < kSR; ++q) {
@@ -1468,6 +1510,7 @@ __global__ void __launch_bounds__(CTBlock<RP>::v) cpass_tile_kernel(
   for (int i = threadIdx.x; i < nbins; i += blockDim.x) El[i] = E_.e[i];
   __syncthreads();
   STAMP(wg, 1);
+  if (ct && u < U) unit_cols();
 
   // 3. units: likelihood + gradient over the part lists
   for (; u < U; u += NW) {
@@ -1498,7 +1541,7 @@ __global__ void __launch_bounds__(CTBlock<RP>::v) cpass_tile_kernel(
       }
       if (lane == 0) Nl[u] = nll_w;
     }
-    if (u + NW < U) unit_begin(u + NW);
+    if (u + NW < U) unit_begin(u + NW, true);
   }
   STAMP(wg, 2);
 
@@ -2766,13 +2809,21 @@ static int cpass_impl(const qsc_obs_desc* d, const void* c_entries, const int32_
     int NP = 1;
     const bool tile = tile_parts(d, R, sr, &NP);
     const int U = nks * NP;
-    const size_t tshm = cpass_tile_lds(d->PT, R, nks, NP, sr);
+    size_t tshm = cpass_tile_lds(d->PT, R, nks, NP, sr);
     if (tile) {
       const dim3 tb((unsigned)(64 * std::min(U, RP > 8 ? QSC_CTILE_W16 : QSC_CTILE_MAXW)));
+      // C^T staged in LDS when it fits next to the tile and in the threads' registers (kCT = 4
+      // floats each): the units' C columns then come from LDS, not from a read that depends on
+      // the bin map (the partition -- tile_parts -- is sized without it)
+      const size_t ct_bytes = 16 + (size_t)d->K * RP * 4;  // [K][RP] (+ alignment)
+      const int ct = (QSC_CTILE_CT && (int64_t)R * d->K <= 4 * (int64_t)tb.x &&
+                      tshm + ct_bytes <= 160 * 1024) ? 1 : 0;
+      if (ct) tshm += ct_bytes;
 #define CPASS_TILE_LAUNCH(RPV, ET, KD, LG)                                                     \
   hipLaunchKernelGGL((cpass_tile_kernel<RPV, ET, KD, LG>), dim3((unsigned)d->ntiles), tb, tshm, \
                      s, (const ET*)c_entries, c_width, c_off, c_kmap, nks, NP, d->PT, lk, E,     \
-                     d->nbins, R, d->K, S, C, w.slab, w.cnll, w.cnsq, nsq ? w.snsq : nullptr)
+                     d->nbins, R, d->K, ct, S, C, w.slab, w.cnll, w.cnsq,                      \
+                     nsq ? w.snsq : nullptr)
       QSC_DISPATCH_PASS(CPASS_TILE_LAUNCH);
 #undef CPASS_TILE_LAUNCH
       QSC_CHECK_LAUNCH();

@@ -76,6 +76,23 @@ def issue_iterations(solver, n):
             solver.iteration()
 
 
+# RCCL's watchdog thread (torch ProcessGroupNCCL) polls the completion events of the eager
+# collectives still on its list every ~100 ms.  Polled while the collectives' stream is being
+# captured, such an event fails the query ("operation not permitted on an event last recorded in
+# a capturing stream") and the watchdog aborts the process -- seen on MI355X when a capture
+# followed an eager collective within milliseconds (profiles/r06/capture_watchdog_abort.log).
+# Before capturing collectives: drain the device, then let the watchdog retire its list.
+CAPTURE_QUIESCE_S = 0.3
+
+
+def quiesce_collectives(dist):
+    if dist is None or not dist.is_initialized() or dist.get_backend() != "nccl":
+        return
+    import time
+    torch.cuda.synchronize()
+    time.sleep(CAPTURE_QUIESCE_S)
+
+
 def _capture(solver, n, tolerant):
     """Capture run(n)'s kernel sequence into a hipGraph on a side stream.
 
@@ -87,6 +104,7 @@ def _capture(solver, n, tolerant):
     is capturing").  Then, for a tolerant solver, the failure is recorded in `graph_error`, the
     solver is marked not capturable and runs eagerly from then on; otherwise the error is
     re-raised.  If the capture cannot be ended the error is always raised."""
+    quiesce_collectives(getattr(solver, "dist", None))
     g = torch.cuda.CUDAGraph()
     s = capture_stream()
     caller = torch.cuda.current_stream()
@@ -94,7 +112,10 @@ def _capture(solver, n, tolerant):
     mark = solver.chain_mark() if hasattr(solver, "chain_mark") else None
     try:
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
+            # thread-local capture mode: other threads' HIP calls (RCCL's watchdog queries the
+            # events of collectives issued before the capture) must neither fail nor invalidate
+            # it -- in the default global mode the watchdog's query errors and aborts the process
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 issue_iterations(solver, n)
     except Exception as e:  # noqa: BLE001 - every failure takes the same clean-up path
         if mark is not None:
@@ -661,7 +682,8 @@ class GeneratorSolver:
         gen0 = self.engine.gen
         try:
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s, pool=self._pool):
+                with torch.cuda.graph(g, stream=s, pool=self._pool,
+                                      capture_error_mode="thread_local"):
                     for _ in range(m):
                         self.iteration()
         except Exception as e:  # noqa: BLE001 - every failure takes the same clean-up path
