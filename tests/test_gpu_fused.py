@@ -159,7 +159,10 @@ def test_solver_graph_replay_matches_eager():
                           (52, 4, 64, 64, 64, False, "probit", 2, 128),
                           (53, 4, 96, 64, 64, False, "probit", 2, None),
                           # C3 shape class at 1024-position tiles
-                          (55, 8, 128, 128, 256, False, "probit", 2, 1024)])
+                          (55, 8, 128, 128, 256, False, "probit", 2, 1024),
+                          # C4 shape class: 16 k-slices, more bins than the 8-wave workgroup
+                          # has threads (the C units' bin map staged in a loop)
+                          (56, 16, 32, 32, 1024, False, "probit", 2, 512)])
 def test_fused_spass_cpass_bitexact(seed, R, I, J, K, log_model, loss, nbins, tile):
     """qsc_scpass (S-step + next C-pass in one launch) reproduces spass + cpass bit for bit:
     S, C and the cost history after n iterations, eager and hipGraph."""
